@@ -1,0 +1,87 @@
+"""Build libdivrec_hip.so (the C-ABI HIP library) in-tree for gfx950.
+
+    python diversity-recommendations_amd/build_native.py [--jobs N] [--verbose]
+
+Each csrc/*.hip file is compiled to an object with hipcc --offload-arch=gfx950
+(cross-compiles without a GPU), then linked into divrec/_lib/libdivrec_hip.so.
+Objects are rebuilt only when a source or header is newer.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG_ROOT = Path(__file__).resolve().parent
+CSRC = PKG_ROOT / "csrc"
+INCLUDE = PKG_ROOT.parent / "include"
+OBJ_DIR = PKG_ROOT / "build" / "obj"
+LIB_DIR = PKG_ROOT / "divrec" / "_lib"
+LIB_PATH = LIB_DIR / "libdivrec_hip.so"
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+CFLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-fPIC",
+    "-std=c++17",
+    "-munsafe-fp-atomics",
+    f"-I{INCLUDE}",
+    f"-I{CSRC}",
+]
+
+
+def _headers_mtime() -> float:
+    hs = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
+    return max((h.stat().st_mtime for h in hs), default=0.0)
+
+
+def _compile(src: Path, verbose: bool) -> Path:
+    obj = OBJ_DIR / (src.stem + ".o")
+    if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
+        return obj
+    cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(jobs: int = 4, verbose: bool = False) -> Path:
+    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    srcs = sorted(CSRC.glob("*.hip"))
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
+    newest = max(o.stat().st_mtime for o in objs)
+    if LIB_PATH.exists() and LIB_PATH.stat().st_mtime >= newest:
+        return LIB_PATH
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+    path = build(args.jobs, args.verbose)
+    print(path)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

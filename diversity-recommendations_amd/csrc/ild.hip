@@ -1,0 +1,293 @@
+// Intra-list diversity: IntraListDiversityScore.recommendations_loss
+// (reference divrec/losses/intra_list_diversity_score.py:20-42) with
+// reduction 'none':  out[u] = (sum_{p<q} D[r[u,p], r[u,q]]) / (k*(k-1)).
+//
+// Three ways to supply D:
+//   * dense matrix (small catalogs, bit-exact parity): fp32 D is accumulated
+//     sequentially in itertools.combinations order in fp32, exactly as the
+//     reference's Python sum() over 0-d tensors (:40-42); integer D is summed
+//     exactly. One lane per user for float D (the order is the contract),
+//     one wave per user for integer D.
+//   * label equality D[i,j] = (label[i] == label[j]) — the matrix built by
+//     IntraListBinaryUnfairnessScore.get_distance_matrix (:60-63) — counted
+//     exactly on the fly; no I x I matrix.
+//   * item embeddings (any catalog size): per user the k rows are gathered
+//     into MFMA fragments and the k x k Gram matrix is formed tile by tile
+//     with v_mfma_f32_32x32x16_bf16; cosine / dot / euclidean distances are
+//     summed over the strict upper triangle. HBM-bound at k=10 (gather of
+//     k*d*2 bytes per user), MFMA-light at k=100.
+#include "common.h"
+
+namespace {
+
+using dr::bf16x8;
+using dr::f32x16;
+
+template <typename R>
+__device__ __forceinline__ int64_t rec_at(const R* recs, int64_t i) {
+  return (int64_t)recs[i];
+}
+
+// --------------------------------------------------------------- dense, float
+template <typename R, typename T, typename ACC>
+__global__ __launch_bounds__(256) void ild_dense_seq(const R* __restrict__ recs, int64_t n_users,
+                                                     int k, const T* __restrict__ D,
+                                                     int64_t n_items, float* __restrict__ out) {
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (u >= n_users) return;
+  const R* r = recs + u * k;
+  ACC acc = 0;
+  for (int p = 0; p < k; ++p) {
+    const T* row = D + rec_at(r, p) * n_items;
+    for (int q = p + 1; q < k; ++q) acc += row[rec_at(r, q)];
+  }
+  out[u] = (float)acc / (float)(k * (k - 1));
+}
+
+// --------------------------------------------------------------- dense, integer
+template <typename R, typename T>
+__global__ __launch_bounds__(256) void ild_dense_int(const R* __restrict__ recs, int64_t n_users,
+                                                     int k, const T* __restrict__ D,
+                                                     int64_t n_items, float* __restrict__ out) {
+  const int lane = dr::lane_id();
+  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (u >= n_users) return;
+  const R* r = recs + u * k;
+  long long acc = 0;
+  for (int p = 0; p < k; ++p) {
+    const T* row = D + rec_at(r, p) * n_items;
+    for (int q = p + 1 + lane; q < k; q += 64) acc += (long long)row[rec_at(r, q)];
+  }
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
+  if (lane == 0) out[u] = (float)acc / (float)(k * (k - 1));
+}
+
+// --------------------------------------------------------------- labels
+constexpr int kLabelMaxK = 1024;
+template <typename R>
+__global__ __launch_bounds__(256) void ild_labels_kernel(const R* __restrict__ recs,
+                                                         int64_t n_users, int k,
+                                                         const int64_t* __restrict__ labels,
+                                                         float* __restrict__ out) {
+  __shared__ int64_t s_lab[4][kLabelMaxK];
+  const int lane = dr::lane_id();
+  const int wave = threadIdx.x >> 6;
+  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (u >= n_users) return;  // wave-uniform; no block barrier below
+  const R* r = recs + u * k;
+  int64_t* lab = s_lab[wave];
+  for (int p = lane; p < k; p += 64) lab[p] = labels[rec_at(r, p)];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  long long cnt = 0;
+  for (int p = lane; p < k; p += 64) {
+    const int64_t lp = lab[p];
+    for (int q = p + 1; q < k; ++q) cnt += (lab[q] == lp);
+  }
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) cnt += __shfl_xor(cnt, m);
+  if (lane == 0) out[u] = (float)cnt / (float)(k * (k - 1));
+}
+
+// --------------------------------------------------------------- embeddings
+// One wave per user. Tile t holds rows [32t, 32t+32) of the user's list as
+// MFMA fragments: lane l -> row (l & 31), k-slice 8*(l >> 5) + 16*s. The same
+// fragment serves as A (rows) and B (columns) operand of X * X^T.
+template <int D>
+__device__ __forceinline__ void load_tile(const __bf16* __restrict__ E, const int64_t* rows,
+                                          int t, int k, bf16x8 (&f)[D / 16]) {
+  const int lane = dr::lane_id();
+  const int p = 32 * t + (lane & 31);
+  const int64_t row = rows[p < k ? p : 0];
+  const uint4* src = reinterpret_cast<const uint4*>(E + row * D + 8 * (lane >> 5));
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) f[s] = __builtin_bit_cast(bf16x8, src[2 * s]);
+}
+
+template <int D>
+__device__ __forceinline__ f32x16 gram_tile(const bf16x8 (&x)[D / 16], const bf16x8 (&y)[D / 16]) {
+  f32x16 acc = f32x16{};
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s)
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[s], y[s], acc, 0, 0, 0);
+  return acc;
+}
+
+constexpr int kEmbMaxK = 128;
+
+template <typename R, int D>
+__global__ __launch_bounds__(256) void ild_embedding_kernel(const R* __restrict__ recs,
+                                                            int64_t n_users, int k,
+                                                            const __bf16* __restrict__ E,
+                                                            int kind, float* __restrict__ out) {
+  __shared__ int64_t s_rows[4][kEmbMaxK];
+  __shared__ float s_nsq[4][kEmbMaxK];
+  const int lane = dr::lane_id();
+  const int wave = threadIdx.x >> 6;
+  const int h = lane >> 5, col = lane & 31;
+  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (u >= n_users) return;  // wave-uniform
+  const R* r = recs + u * k;
+  int64_t* rows = s_rows[wave];
+  float* nsq = s_nsq[wave];
+  for (int p = lane; p < k; p += 64) rows[p] = rec_at(r, p);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int nt = (k + 31) / 32;
+
+  // Squared norms from the diagonal tiles: element (row == col) sits in the
+  // lane with col = j and register r = (j & 3) + 4 * (j >> 3) when (j >> 2) & 1 == h.
+  for (int t = 0; t < nt; ++t) {
+    bf16x8 x[D / 16];
+    load_tile<D>(E, rows, t, k, x);
+    const f32x16 g = gram_tile<D>(x, x);
+    const int ri = (col & 3) + 4 * (col >> 3);
+    float v = g[0];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) v = (ri == q) ? g[q] : v;
+    if (((col >> 2) & 1) == h) nsq[32 * t + col] = v;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  float sum = 0.f;
+  for (int ti = 0; ti < nt; ++ti) {
+    bf16x8 x[D / 16];
+    load_tile<D>(E, rows, ti, k, x);
+    for (int tj = ti; tj < nt; ++tj) {
+      bf16x8 y[D / 16];
+      load_tile<D>(E, rows, tj, k, y);
+      const f32x16 g = gram_tile<D>(x, y);  // g[r] = <e_i, e_j>, i = row, j = col
+      const int j = 32 * tj + col;
+      const float nj = j < k ? nsq[j] : 1.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = 32 * ti + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (i < j && j < k) {
+          const float ni = nsq[i];
+          float dist;
+          if (kind == DR_ILD_COSINE) dist = 1.f - g[q] / (sqrtf(ni) * sqrtf(nj));
+          else if (kind == DR_ILD_DOT) dist = g[q];
+          else dist = sqrtf(fmaxf(ni + nj - 2.f * g[q], 0.f));
+          sum += dist;
+        }
+      }
+    }
+  }
+  sum = dr::wave_sum_f32(sum);
+  if (lane == 0) out[u] = sum / (float)(k * (k - 1));
+}
+
+template <typename R>
+int launch_embedding(const R* recs, int64_t n_users, int k, const __bf16* E, int d, int kind,
+                     float* out, hipStream_t s) {
+  const int grid = (int)dr::ceil_div(n_users, 4);
+  switch (d) {
+    case 32: hipLaunchKernelGGL((ild_embedding_kernel<R, 32>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
+    case 64: hipLaunchKernelGGL((ild_embedding_kernel<R, 64>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
+    case 128: hipLaunchKernelGGL((ild_embedding_kernel<R, 128>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
+    case 256: hipLaunchKernelGGL((ild_embedding_kernel<R, 256>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
+    default:
+      dr::set_error("dr_ild_embedding: d must be one of 32, 64, 128, 256");
+      return DR_EUNSUPPORTED;
+  }
+  return DR_OK;
+}
+
+template <typename R>
+int launch_dense(const R* recs, int64_t n_users, int k, const void* D, int dd, int64_t n_items,
+                 float* out, hipStream_t s) {
+  switch (dd) {
+    case DR_F32: {
+      const int grid = (int)dr::ceil_div(n_users, 256);
+      hipLaunchKernelGGL((ild_dense_seq<R, float, float>), grid, 256, 0, s, recs, n_users, k,
+                         (const float*)D, n_items, out);
+      break;
+    }
+    case DR_F64: {
+      const int grid = (int)dr::ceil_div(n_users, 256);
+      hipLaunchKernelGGL((ild_dense_seq<R, double, double>), grid, 256, 0, s, recs, n_users, k,
+                         (const double*)D, n_items, out);
+      break;
+    }
+    case DR_I32: {
+      const int grid = (int)dr::ceil_div(n_users, 4);
+      hipLaunchKernelGGL((ild_dense_int<R, int32_t>), grid, 256, 0, s, recs, n_users, k,
+                         (const int32_t*)D, n_items, out);
+      break;
+    }
+    case DR_I64: {
+      const int grid = (int)dr::ceil_div(n_users, 4);
+      hipLaunchKernelGGL((ild_dense_int<R, int64_t>), grid, 256, 0, s, recs, n_users, k,
+                         (const int64_t*)D, n_items, out);
+      break;
+    }
+    default:
+      dr::set_error("dr_ild_dense: dist dtype must be DR_F32, DR_F64, DR_I32 or DR_I64");
+      return DR_EUNSUPPORTED;
+  }
+  return DR_OK;
+}
+
+}  // namespace
+
+extern "C" int dr_ild_dense(const void* recs, int rec_dtype, int64_t n_users, int k,
+                            const void* dist, int dist_dtype, int64_t n_items, float* out,
+                            dr_stream_t stream) {
+  DR_CHECK_ARG(k >= 1, "k must be >= 1");
+  DR_CHECK_ARG(rec_dtype == DR_I32 || rec_dtype == DR_I64, "rec_dtype must be DR_I32/DR_I64");
+  if (n_users == 0) return DR_OK;
+  DR_CHECK_ARG(recs && dist && out, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  int rc = rec_dtype == DR_I32
+               ? launch_dense((const int32_t*)recs, n_users, k, dist, dist_dtype, n_items, out, s)
+               : launch_dense((const int64_t*)recs, n_users, k, dist, dist_dtype, n_items, out, s);
+  if (rc != DR_OK) return rc;
+  DR_CHECK_LAUNCH();
+  return DR_OK;
+}
+
+extern "C" int dr_ild_labels(const void* recs, int rec_dtype, int64_t n_users, int k,
+                             const int64_t* labels, int64_t n_items, float* out,
+                             dr_stream_t stream) {
+  DR_CHECK_ARG(k >= 1 && k <= kLabelMaxK, "k must be in [1, 1024]");
+  DR_CHECK_ARG(rec_dtype == DR_I32 || rec_dtype == DR_I64, "rec_dtype must be DR_I32/DR_I64");
+  (void)n_items;
+  if (n_users == 0) return DR_OK;
+  DR_CHECK_ARG(recs && labels && out, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = (int)dr::ceil_div(n_users, 4);
+  if (rec_dtype == DR_I32)
+    hipLaunchKernelGGL((ild_labels_kernel<int32_t>), grid, 256, 0, s, (const int32_t*)recs,
+                       n_users, k, labels, out);
+  else
+    hipLaunchKernelGGL((ild_labels_kernel<int64_t>), grid, 256, 0, s, (const int64_t*)recs,
+                       n_users, k, labels, out);
+  DR_CHECK_LAUNCH();
+  return DR_OK;
+}
+
+extern "C" int dr_ild_embedding(const void* recs, int rec_dtype, int64_t n_users, int k,
+                                const void* item_table, int64_t n_items, int d, int kind,
+                                float* out, dr_stream_t stream) {
+  DR_CHECK_ARG(k >= 1 && k <= kEmbMaxK, "k must be in [1, 128]");
+  DR_CHECK_ARG(rec_dtype == DR_I32 || rec_dtype == DR_I64, "rec_dtype must be DR_I32/DR_I64");
+  DR_CHECK_ARG(kind == DR_ILD_COSINE || kind == DR_ILD_DOT || kind == DR_ILD_EUCLIDEAN,
+               "unknown distance kind");
+  (void)n_items;
+  if (n_users == 0) return DR_OK;
+  DR_CHECK_ARG(recs && item_table && out, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  int rc = rec_dtype == DR_I32
+               ? launch_embedding((const int32_t*)recs, n_users, k, (const __bf16*)item_table, d,
+                                  kind, out, s)
+               : launch_embedding((const int64_t*)recs, n_users, k, (const __bf16*)item_table, d,
+                                  kind, out, s);
+  if (rc != DR_OK) return rc;
+  DR_CHECK_LAUNCH();
+  return DR_OK;
+}

@@ -1,0 +1,136 @@
+"""ctypes binding of libdivrec_hip.so (C ABI declared in include/divrec_hip.h).
+
+The library is the only compute backend of the divrec hot path: there is no
+CPU fallback. If the shared object is missing, or no ROCm device is visible,
+every call raises ``RuntimeError`` — loudly, never silently degrading.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+from typing import Optional
+
+import torch
+
+LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libdivrec_hip.so"
+
+DR_F32, DR_BF16, DR_I32, DR_I64, DR_F64 = 0, 1, 2, 3, 4
+DR_ILD_COSINE, DR_ILD_DOT, DR_ILD_EUCLIDEAN = 0, 1, 2
+
+_DTYPE_CODE = {
+    torch.float32: DR_F32,
+    torch.bfloat16: DR_BF16,
+    torch.int32: DR_I32,
+    torch.int64: DR_I64,
+    torch.float64: DR_F64,
+}
+
+_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_f32 = ctypes.c_float
+_f64 = ctypes.c_double
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/divrec_hip.h one to one.
+SIGNATURES = {
+    "dr_version": (_i32, []),
+    "dr_last_error": (ctypes.c_char_p, []),
+    "dr_gather_dot": (_i32, [_p, _p, _i32, _i64, _p, _p, _i64, _p, _p]),
+    "dr_gather_dot_backward": (_i32, [_p, _p, _i64, _p, _p, _i64, _p, _p, _p, _p]),
+    "dr_score_topk_workspace": (_sz, [_i64, _i64, _i32, _i32]),
+    "dr_score_topk": (
+        _i32,
+        [_p, _p, _i64, _p, _i64, _i64, _i32, _i32, _p, _p, _p, _p, _p, _sz, _p],
+    ),
+    "dr_topk_merge": (_i32, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p]),
+    "dr_ild_dense": (_i32, [_p, _i32, _i64, _i32, _p, _i32, _i64, _p, _p]),
+    "dr_ild_labels": (_i32, [_p, _i32, _i64, _i32, _p, _i64, _p, _p]),
+    "dr_ild_embedding": (_i32, [_p, _i32, _i64, _i32, _p, _i64, _i32, _i32, _p, _p]),
+    "dr_bpr_fwd_bwd": (_i32, [_p, _p, _i64, _p, _p, _p, _i64, _f32, _p, _p, _p, _p, _p]),
+    "dr_adam_dense": (_i32, [_p, _p, _p, _p, _i64, _f64, _f64, _f64, _f64, _f64, _i64, _p]),
+    "dr_mmr_rerank": (_i32, [_p, _p, _i64, _i32, _p, _i64, _i32, _i32, _f32, _p, _p]),
+}
+
+_LIB: Optional[ctypes.CDLL] = None
+
+
+def lib_path() -> Path:
+    return Path(os.environ.get("DIVREC_HIP_LIB", str(LIB_PATH)))
+
+
+def load_library() -> ctypes.CDLL:
+    """Load the shared object (no device needed) and declare every symbol."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not path.exists():
+        raise RuntimeError(
+            f"divrec HIP backend not built: {path} is missing. "
+            "Run `python diversity-recommendations_amd/build_native.py`."
+        )
+    # torch (imported above) has already loaded its HIP runtime; the library's
+    # libamdhip64.so.7 dependency resolves to that same copy by SONAME.
+    lib = ctypes.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def lib() -> ctypes.CDLL:
+    return load_library()
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        msg = lib().dr_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
+def require_device(*tensors: torch.Tensor) -> torch.device:
+    """All tensors must live on one ROCm device; returns it."""
+    if not torch.cuda.is_available():
+        raise RuntimeError(
+            "divrec HIP backend requires a ROCm GPU (torch.cuda.is_available() is False); "
+            "there is no CPU fallback"
+        )
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError(f"expected a tensor on a ROCm device, got {t.device}")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"tensors on different devices: {dev} vs {t.device}")
+    return dev if dev is not None else torch.device("cuda", torch.cuda.current_device())
+
+
+def default_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError(
+            "divrec HIP backend requires a ROCm GPU (torch.cuda.is_available() is False); "
+            "there is no CPU fallback"
+        )
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    try:
+        return _DTYPE_CODE[dt]
+    except KeyError:
+        raise RuntimeError(f"unsupported dtype {dt}") from None

@@ -1,0 +1,306 @@
+"""Tensor-level entry points of the HIP hot path (one function per C-ABI call).
+
+Every function takes device tensors, validates dtype / shape / contiguity on
+the host, and enqueues the HIP kernel on the current stream of the tensors'
+device. Outputs are freshly allocated by the PyTorch caching allocator; the
+native library never allocates. There is no CPU implementation here.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from divrec import _backend as B
+
+
+def _contig(t: torch.Tensor, name: str) -> torch.Tensor:
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t
+
+
+def _need(cond: bool, msg: str) -> None:
+    if not cond:
+        raise ValueError(msg)
+
+
+# --------------------------------------------------------------------------- MF forward
+def gather_dot(
+    user_table: torch.Tensor,
+    item_table: torch.Tensor,
+    user_id: torch.Tensor,
+    item_id: torch.Tensor,
+) -> torch.Tensor:
+    """s[n] = <U[user_id[n]], I[item_id[n]]> (MatrixFactorization.forward,
+    reference divrec/models/matrix_factorization.py:26-28). fp32 or bf16 tables,
+    int64 ids, fp32 output."""
+    dev = B.require_device(user_table, item_table, user_id, item_id)
+    _need(user_table.dim() == 2 and item_table.dim() == 2, "tables must be 2-D")
+    _need(user_table.size(1) == item_table.size(1), "tables must share embedding_dim")
+    _need(user_table.dtype == item_table.dtype, "tables must share dtype")
+    _need(user_table.dtype in (torch.float32, torch.bfloat16), "tables must be fp32 or bf16")
+    _need(user_id.dtype == torch.int64 and item_id.dtype == torch.int64, "ids must be int64")
+    _need(user_id.dim() == 1 and user_id.shape == item_id.shape, "ids must be 1-D, same length")
+    _contig(user_table, "user_table"), _contig(item_table, "item_table")
+    user_id, item_id = user_id.contiguous(), item_id.contiguous()
+    out = torch.empty(user_id.numel(), dtype=torch.float32, device=dev)
+    rc = B.lib().dr_gather_dot(
+        user_table.data_ptr(), item_table.data_ptr(), B.dtype_code(user_table.dtype),
+        user_table.size(1), user_id.data_ptr(), item_id.data_ptr(), user_id.numel(),
+        out.data_ptr(), B.stream(dev),
+    )
+    B.check(rc, "dr_gather_dot")
+    return out
+
+
+def gather_dot_backward(
+    user_table: torch.Tensor,
+    item_table: torch.Tensor,
+    user_id: torch.Tensor,
+    item_id: torch.Tensor,
+    grad_out: torch.Tensor,
+    grad_user: Optional[torch.Tensor],
+    grad_item: Optional[torch.Tensor],
+) -> None:
+    """Accumulate dense fp32 embedding gradients of gather_dot in place."""
+    dev = B.require_device(user_table, item_table, user_id, item_id, grad_out, grad_user, grad_item)
+    _need(user_table.dtype == torch.float32 and item_table.dtype == torch.float32,
+          "backward needs fp32 tables")
+    for g, t, nm in ((grad_user, user_table, "grad_user"), (grad_item, item_table, "grad_item")):
+        if g is not None:
+            _need(g.shape == t.shape and g.dtype == torch.float32 and g.is_contiguous(),
+                  f"{nm} must be a contiguous fp32 tensor shaped like its table")
+    grad_out = grad_out.to(torch.float32).contiguous()
+    rc = B.lib().dr_gather_dot_backward(
+        user_table.data_ptr(), item_table.data_ptr(), user_table.size(1),
+        user_id.contiguous().data_ptr(), item_id.contiguous().data_ptr(), user_id.numel(),
+        grad_out.data_ptr(), B.ptr(grad_user), B.ptr(grad_item), B.stream(dev),
+    )
+    B.check(rc, "dr_gather_dot_backward")
+
+
+# --------------------------------------------------------------------------- top-K
+def score_topk(
+    user_table: torch.Tensor,
+    item_table: torch.Tensor,
+    k: int,
+    user_ids: Optional[torch.Tensor] = None,
+    n_users: Optional[int] = None,
+    item_base: int = 0,
+    exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Top-k items per user over the catalog slice ``item_table`` (global ids
+    ``item_base + row``) by bf16 MFMA scores; order = score desc, item id asc.
+
+    ``user_ids`` (int64) selects user rows; if None the first ``n_users`` rows
+    (default: all) are scored. ``exclude = (rowptr int64 [n+1], items int32)``
+    is a CSR of GLOBAL item ids (sorted per row) never to recommend.
+    Returns (scores fp32 [n, k], items int32 [n, k]).
+    """
+    dev = B.require_device(user_table, item_table, user_ids)
+    _need(user_table.dtype == torch.bfloat16 and item_table.dtype == torch.bfloat16,
+          "score_topk runs on bf16 tables (convert with .to(torch.bfloat16))")
+    _need(user_table.dim() == 2 and item_table.dim() == 2, "tables must be 2-D")
+    d = user_table.size(1)
+    _need(item_table.size(1) == d, "tables must share embedding_dim")
+    _need(d in (32, 64, 128, 256), "embedding_dim must be one of 32, 64, 128, 256")
+    _contig(user_table, "user_table"), _contig(item_table, "item_table")
+    _need(1 <= k <= 1024, "k must be in [1, 1024]")
+    if user_ids is not None:
+        _need(user_ids.dtype == torch.int64 and user_ids.dim() == 1, "user_ids must be 1-D int64")
+        user_ids = user_ids.contiguous()
+        n = user_ids.numel()
+        if n:
+            lo, hi = int(user_ids.min()), int(user_ids.max())
+            _need(0 <= lo and hi < user_table.size(0), "user_ids out of range")
+    else:
+        n = user_table.size(0) if n_users is None else int(n_users)
+        _need(0 <= n <= user_table.size(0), "n_users out of range")
+    n_items = item_table.size(0)
+    _need(k <= n_items or exclude is not None or n_items == 0, "k must be <= number of items")
+    rowptr = cols = None
+    if exclude is not None:
+        rowptr, cols = exclude
+        B.require_device(rowptr, cols)
+        _need(rowptr.dtype == torch.int64 and rowptr.numel() == n + 1, "rowptr must be int64 [n+1]")
+        _need(cols.dtype == torch.int32, "excluded items must be int32")
+        rowptr, cols = rowptr.contiguous(), cols.contiguous()
+        if cols.numel() == 0:
+            cols = torch.zeros(1, dtype=torch.int32, device=dev)
+    scores = torch.empty((n, k), dtype=torch.float32, device=dev)
+    items = torch.empty((n, k), dtype=torch.int32, device=dev)
+    if n == 0:
+        return scores, items
+    L = B.lib()
+    ws_bytes = L.dr_score_topk_workspace(n, n_items, d, k)
+    ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=dev)
+    rc = L.dr_score_topk(
+        user_table.data_ptr(), B.ptr(user_ids), n, item_table.data_ptr(), n_items, int(item_base),
+        d, int(k), B.ptr(rowptr), B.ptr(cols), scores.data_ptr(), items.data_ptr(),
+        ws.data_ptr(), ws.numel(), B.stream(dev),
+    )
+    B.check(rc, "dr_score_topk")
+    return scores, items
+
+
+def topk_merge(
+    scores: torch.Tensor, items: torch.Tensor, k_out: Optional[int] = None
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Merge per-part sorted top-k lists [parts, n, k_in] -> [n, k_out]."""
+    dev = B.require_device(scores, items)
+    _need(scores.dim() == 3 and scores.shape == items.shape, "expected [parts, n, k] inputs")
+    _need(scores.dtype == torch.float32 and items.dtype == torch.int32, "fp32 scores, int32 items")
+    parts, n, k_in = scores.shape
+    k_out = k_in if k_out is None else int(k_out)
+    _need(1 <= k_out <= parts * k_in and parts * k_in <= 2048, "k_out / parts*k_in out of range")
+    out_s = torch.empty((n, k_out), dtype=torch.float32, device=dev)
+    out_i = torch.empty((n, k_out), dtype=torch.int32, device=dev)
+    if n == 0:
+        return out_s, out_i
+    rc = B.lib().dr_topk_merge(
+        scores.contiguous().data_ptr(), items.contiguous().data_ptr(), parts, n, k_in, k_out,
+        out_s.data_ptr(), out_i.data_ptr(), B.stream(dev),
+    )
+    B.check(rc, "dr_topk_merge")
+    return out_s, out_i
+
+
+# --------------------------------------------------------------------------- ILD
+def _recs(recs: torch.Tensor) -> Tuple[torch.Tensor, int]:
+    _need(recs.dim() == 2, "recommendations must be [n_users, k]")
+    _need(recs.dtype in (torch.int32, torch.int64), "recommendations must be int32 or int64")
+    return recs.contiguous(), B.dtype_code(recs.dtype)
+
+
+def ild_dense(recs: torch.Tensor, dist: torch.Tensor) -> torch.Tensor:
+    """Per-user ILD against a dense [I, I] distance matrix (fp32/fp64/int32/int64)."""
+    dev = B.require_device(recs, dist)
+    recs, rc_dt = _recs(recs)
+    _need(dist.dim() == 2 and dist.size(0) == dist.size(1), "distance matrix must be [I, I]")
+    _need(dist.dtype in (torch.float32, torch.float64, torch.int32, torch.int64),
+          "distance matrix dtype must be float32/float64/int32/int64")
+    dist = dist.contiguous()
+    n, k = recs.shape
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    if n == 0:
+        return out
+    rc = B.lib().dr_ild_dense(
+        recs.data_ptr(), rc_dt, n, k, dist.data_ptr(), B.dtype_code(dist.dtype), dist.size(0),
+        out.data_ptr(), B.stream(dev),
+    )
+    B.check(rc, "dr_ild_dense")
+    return out
+
+
+def ild_labels(recs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """Per-user ILD with D[i,j] = (labels[i] == labels[j]) computed on the fly."""
+    dev = B.require_device(recs, labels)
+    recs, rc_dt = _recs(recs)
+    labels = labels.to(torch.int64).contiguous()
+    n, k = recs.shape
+    _need(k <= 1024, "k must be <= 1024")
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    if n == 0:
+        return out
+    rc = B.lib().dr_ild_labels(
+        recs.data_ptr(), rc_dt, n, k, labels.data_ptr(), labels.numel(), out.data_ptr(),
+        B.stream(dev),
+    )
+    B.check(rc, "dr_ild_labels")
+    return out
+
+
+_KINDS = {"cosine": B.DR_ILD_COSINE, "dot": B.DR_ILD_DOT, "euclidean": B.DR_ILD_EUCLIDEAN}
+
+
+def ild_embedding(recs: torch.Tensor, item_table: torch.Tensor, kind: str = "cosine") -> torch.Tensor:
+    """Per-user ILD with D computed from bf16 item embeddings (cosine/dot/euclidean)."""
+    dev = B.require_device(recs, item_table)
+    recs, rc_dt = _recs(recs)
+    _need(item_table.dtype == torch.bfloat16 and item_table.dim() == 2, "item_table must be bf16 2-D")
+    _contig(item_table, "item_table")
+    _need(kind in _KINDS, f"kind must be one of {sorted(_KINDS)}")
+    n, k = recs.shape
+    _need(k <= 128, "embedding ILD supports k <= 128")
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    if n == 0:
+        return out
+    rc = B.lib().dr_ild_embedding(
+        recs.data_ptr(), rc_dt, n, k, item_table.data_ptr(), item_table.size(0),
+        item_table.size(1), _KINDS[kind], out.data_ptr(), B.stream(dev),
+    )
+    B.check(rc, "dr_ild_embedding")
+    return out
+
+
+# --------------------------------------------------------------------------- BPR
+def bpr_fwd_bwd(
+    user_table: torch.Tensor,
+    item_table: torch.Tensor,
+    user_id: torch.Tensor,
+    pos_id: torch.Tensor,
+    neg_id: torch.Tensor,
+    grad_scale: float,
+    grad_user: Optional[torch.Tensor],
+    grad_item: Optional[torch.Tensor],
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Fused BPR forward + backward; returns per-triple (loss fp32, hit int32)
+    and accumulates dense gradients into grad_user / grad_item."""
+    dev = B.require_device(user_table, item_table, user_id, pos_id, neg_id, grad_user, grad_item)
+    _need(user_table.dtype == torch.float32 and item_table.dtype == torch.float32, "fp32 tables")
+    for t in (user_id, pos_id, neg_id):
+        _need(t.dtype == torch.int64 and t.dim() == 1 and t.numel() == user_id.numel(),
+              "ids must be 1-D int64 of equal length")
+    n = user_id.numel()
+    loss = torch.empty(n, dtype=torch.float32, device=dev)
+    hit = torch.empty(n, dtype=torch.int32, device=dev)
+    rc = B.lib().dr_bpr_fwd_bwd(
+        user_table.data_ptr(), item_table.data_ptr(), user_table.size(1),
+        user_id.contiguous().data_ptr(), pos_id.contiguous().data_ptr(),
+        neg_id.contiguous().data_ptr(), n, float(grad_scale), loss.data_ptr(), hit.data_ptr(),
+        B.ptr(grad_user), B.ptr(grad_item), B.stream(dev),
+    )
+    B.check(rc, "dr_bpr_fwd_bwd")
+    return loss, hit
+
+
+def adam_dense(
+    param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
+    lr: float, beta1: float, beta2: float, eps: float, weight_decay: float, step: int,
+) -> None:
+    dev = B.require_device(param, grad, exp_avg, exp_avg_sq)
+    for t in (param, grad, exp_avg, exp_avg_sq):
+        _need(t.dtype == torch.float32 and t.is_contiguous() and t.numel() == param.numel(),
+              "adam tensors must be contiguous fp32 of equal size")
+    rc = B.lib().dr_adam_dense(
+        param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+        param.numel(), float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
+        int(step), B.stream(dev),
+    )
+    B.check(rc, "dr_adam_dense")
+
+
+# --------------------------------------------------------------------------- MMR
+def mmr_rerank(
+    cand_items: torch.Tensor, cand_scores: torch.Tensor, item_table: torch.Tensor, k_out: int,
+    lam: float = 0.5,
+) -> torch.Tensor:
+    """Greedy MMR over per-user candidates (int32 [n, C] + fp32 [n, C]) -> int32 [n, k_out]."""
+    dev = B.require_device(cand_items, cand_scores, item_table)
+    _need(cand_items.dtype == torch.int32 and cand_scores.dtype == torch.float32,
+          "int32 candidate ids, fp32 scores")
+    _need(cand_items.dim() == 2 and cand_items.shape == cand_scores.shape, "[n, C] inputs")
+    _need(item_table.dtype == torch.bfloat16 and item_table.size(1) in (64, 128),
+          "item_table must be bf16 with d in {64, 128}")
+    n, C = cand_items.shape
+    out = torch.empty((n, int(k_out)), dtype=torch.int32, device=dev)
+    if n == 0:
+        return out
+    rc = B.lib().dr_mmr_rerank(
+        cand_items.contiguous().data_ptr(), cand_scores.contiguous().data_ptr(), n, C,
+        item_table.contiguous().data_ptr(), item_table.size(0), item_table.size(1), int(k_out),
+        float(lam), out.data_ptr(), B.stream(dev),
+    )
+    B.check(rc, "dr_mmr_rerank")
+    return out

@@ -1,0 +1,175 @@
+/*
+ * libdivrec_hip — C ABI of the MI355X (gfx950) hot path of divrec
+ * (amtsyplov/diversity-recommendations). Plain pointers and sizes only; no
+ * torch types. Every pointer argument is DEVICE memory owned by the caller
+ * unless the comment says otherwise. The library never allocates device
+ * memory: scratch comes from a caller-owned workspace sized by the matching
+ * *_workspace() query. All work is enqueued asynchronously on `stream`
+ * (a hipStream_t; NULL = the legacy default stream).
+ *
+ * Return value: DR_OK (0) or a negative DR_E* code; dr_last_error() then holds
+ * a thread-local message. The Python host (divrec/_backend.py) raises
+ * RuntimeError(dr_last_error()) on any non-zero status.
+ *
+ * Reference entry points each function replaces are cited as
+ * path:line relative to the reference tree (divrec/ ...).
+ */
+#ifndef DIVREC_HIP_H_
+#define DIVREC_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* dr_stream_t; /* hipStream_t */
+
+enum dr_status {
+  DR_OK = 0,
+  DR_EINVAL = -1,       /* bad shape / pointer / argument */
+  DR_EUNSUPPORTED = -2, /* unsupported d / k / dtype combination */
+  DR_EHIP = -3,         /* HIP runtime error (launch failure etc.) */
+  DR_EWORKSPACE = -4    /* workspace too small */
+};
+
+enum dr_dtype { DR_F32 = 0, DR_BF16 = 1, DR_I32 = 2, DR_I64 = 3, DR_F64 = 4 };
+
+enum dr_ild_kind {
+  DR_ILD_COSINE = 0,    /* 1 - <e_i,e_j> / (|e_i| |e_j|) */
+  DR_ILD_DOT = 1,       /* <e_i,e_j> */
+  DR_ILD_EUCLIDEAN = 2  /* |e_i - e_j|_2 */
+};
+
+/* Library version (major*10000 + minor*100 + patch). */
+int dr_version(void);
+/* Thread-local message of the last failing call on this thread ("" if none). */
+const char* dr_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * MatrixFactorization.forward: s[n] = sum_d U[user_id[n], d] * I[item_id[n], d]
+ * Replaces divrec/models/matrix_factorization.py:26-28 (two nn.Embedding
+ * lookups + torch.sum(u * i, dim=1)). Tables row-major [rows, d], dtype
+ * DR_F32 or DR_BF16 (both tables the same dtype); ids int64; out fp32 [n].
+ * Ids are not range-checked on device (the host validates them).
+ */
+int dr_gather_dot(const void* user_table, const void* item_table, int dtype, int64_t d,
+                  const int64_t* user_id, const int64_t* item_id, int64_t n, float* out,
+                  dr_stream_t stream);
+
+/* Backward of dr_gather_dot into DENSE fp32 gradient tables (nn.Embedding with
+ * sparse=False, divrec/models/matrix_factorization.py:16-17):
+ *   grad_user[user_id[n]] += grad_out[n] * I[item_id[n]]
+ *   grad_item[item_id[n]] += grad_out[n] * U[user_id[n]]
+ * Accumulates with fp32 atomics (order-dependent in the last bits). Either
+ * grad pointer may be NULL to skip that table. Tables must be DR_F32. */
+int dr_gather_dot_backward(const float* user_table, const float* item_table, int64_t d,
+                           const int64_t* user_id, const int64_t* item_id, int64_t n,
+                           const float* grad_out, float* grad_user, float* grad_item,
+                           dr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Full-catalog scoring + top-K: for each of the n_users user rows, the k best
+ * items of the catalog slice [item_base, item_base + n_items) by
+ * score = <U[user], I[item]> computed as a bf16 MFMA GEMM with fp32
+ * accumulation. Replaces get_model_recommendations (divrec/train/utils.py:53-77)
+ * over RankingDataset candidates (divrec/datasets/base_datasets.py:136-171).
+ *
+ * Ranking order is score descending, item id ascending (the deterministic
+ * tie-break the reference's unstable argsort leaves undefined, utils.py:73).
+ *
+ *   user_table  bf16 [*, d]; user_ids int64 [n_users] or NULL (rows 0..n_users-1)
+ *   item_table  bf16 [n_items, d] (the rows of THIS slice; global id = item_base + row)
+ *   d in {32, 64, 128, 256}; 1 <= k <= 1024
+ *   excl_rowptr int64 [n_users + 1], excl_items int32 (GLOBAL item ids, sorted
+ *     ascending per row): items excluded per user (RankingDataset `frozen`,
+ *     base_datasets.py:143-149). Both NULL = no exclusion.
+ *   out_scores fp32 [n_users, k], out_items int32 [n_users, k] (GLOBAL ids);
+ *     slots with no candidate hold item -1 and score -inf.
+ *   workspace of dr_score_topk_workspace(...) bytes (query with identical args).
+ */
+size_t dr_score_topk_workspace(int64_t n_users, int64_t n_items, int d, int k);
+int dr_score_topk(const void* user_table, const int64_t* user_ids, int64_t n_users,
+                  const void* item_table, int64_t n_items, int64_t item_base, int d, int k,
+                  const int64_t* excl_rowptr, const int32_t* excl_items, float* out_scores,
+                  int32_t* out_items, void* workspace, size_t workspace_bytes,
+                  dr_stream_t stream);
+
+/* Merge `parts` per-user top-k lists (each sorted by the order above) into one:
+ *   in_scores/in_items [parts, n_users, k_in] -> out [n_users, k_out], k_out <= parts*k_in.
+ * This is the exchange step of the item-row-sharded top-K:
+ * shard partials are all-gathered over RCCL and merged here; the result is
+ * bit-identical to the single-device dr_score_topk over the whole catalog. */
+int dr_topk_merge(const float* in_scores, const int32_t* in_items, int parts, int64_t n_users,
+                  int k_in, int k_out, float* out_scores, int32_t* out_items,
+                  dr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Intra-list diversity, IntraListDiversityScore.recommendations_loss with
+ * reduction 'none' (divrec/losses/intra_list_diversity_score.py:20-42):
+ *   out[u] = (sum_{p<q} D[r[u,p], r[u,q]]) / (k * (k - 1))     (k = 1 -> NaN)
+ * `recs` [n_users, k] item ids of dtype rec_dtype (DR_I32 or DR_I64).
+ */
+
+/* Dense distance matrix D [n_items, n_items] (dtype DR_F32, DR_F64, DR_I32 or
+ * DR_I64). Float D is accumulated in its own precision in itertools.combinations order, like the
+ * reference's Python sum (bit-exact); integer D is summed exactly. */
+int dr_ild_dense(const void* recs, int rec_dtype, int64_t n_users, int k, const void* dist,
+                 int dist_dtype, int64_t n_items, float* out, dr_stream_t stream);
+
+/* Label equality D[i,j] = (label[i] == label[j]), the matrix of
+ * IntraListBinaryUnfairnessScore.get_distance_matrix (:60-63), computed on the
+ * fly from labels int64 [n_items] (exact integer count). */
+int dr_ild_labels(const void* recs, int rec_dtype, int64_t n_users, int k,
+                  const int64_t* labels, int64_t n_items, float* out, dr_stream_t stream);
+
+/* Distance computed on the fly from an item embedding table (bf16 [n_items, d],
+ * d in {32, 64, 128, 256}, k <= 128) by a bf16 MFMA Gram tile per user
+ * (kind: enum dr_ild_kind). fp32 accumulation. */
+int dr_ild_embedding(const void* recs, int rec_dtype, int64_t n_users, int k,
+                     const void* item_table, int64_t n_items, int d, int kind, float* out,
+                     dr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * BPR step (pair_wise_train_loop, divrec/train/utils.py:144-152, with
+ * LogSigmoidDifferenceLoss, divrec/losses/log_sigmoid_difference_loss.py:11-14):
+ *   x[b] = <U[u_b], I[p_b]> - <U[u_b], I[n_b]>
+ *   loss[b] = -logsigmoid(x[b]);  hit[b] = (x_pos >= x_neg) (AUCScore, auc_score.py:6-10)
+ *   g = -sigmoid(-x) * grad_scale  (grad_scale = 1/B for the 'mean' reduction)
+ *   grad_user[u] += g (I[p] - I[n]); grad_item[p] += g U[u]; grad_item[n] -= g U[u]
+ * fp32 tables [*, d]; ids int64 [B]; loss fp32 [B] and hit int32 [B] may be
+ * NULL. Gradients are DENSE fp32 tables accumulated with atomics. */
+int dr_bpr_fwd_bwd(const float* user_table, const float* item_table, int64_t d,
+                   const int64_t* user_id, const int64_t* pos_id, const int64_t* neg_id,
+                   int64_t batch, float grad_scale, float* loss, int32_t* hit,
+                   float* grad_user, float* grad_item, dr_stream_t stream);
+
+/* Dense Adam step in fp32 over n elements, the update torch.optim.Adam
+ * (amsgrad=False, maximize=False) applies at divrec/train/utils.py:151:
+ *   g = grad + weight_decay * param; m = lerp(m, g, 1 - beta1);
+ *   v = beta2 * v + (1 - beta2) * g * g;
+ *   param -= (lr / (1 - beta1^step)) * m / (sqrt(v) / sqrt(1 - beta2^step) + eps)
+ * `step` is the 1-based step count AFTER incrementing. Hyper-parameters are
+ * doubles (Python floats); they are combined in double and cast to fp32 once,
+ * as torch does. */
+int dr_adam_dense(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                  int64_t n, double lr, double beta1, double beta2, double eps,
+                  double weight_decay, int64_t step, dr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * MMR diversity re-rank (config 5; no reference symbol — SURVEY.md §8a a16):
+ * per user, greedily pick k_out of the C candidates maximising
+ *   lambda * score_i - (1 - lambda) * max_{j in S} cos(e_i, e_j)
+ * (ties -> lowest candidate position). cand_items int32 [n_users, C],
+ * cand_scores fp32 [n_users, C], item_table bf16 [*, d]; out int32 [n_users, k_out]
+ * (item ids in selection order). C <= 1024, k_out <= C, d in {64, 128}. */
+int dr_mmr_rerank(const int32_t* cand_items, const float* cand_scores, int64_t n_users, int C,
+                  const void* item_table, int64_t n_items, int d, int k_out, float lambda,
+                  int32_t* out_items, dr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DIVREC_HIP_H_ */

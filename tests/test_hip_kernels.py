@@ -1,0 +1,270 @@
+"""GPU parity tests: every C-ABI kernel against the CPU oracle on seeded inputs.
+
+Integer and byte/index work is checked bit-exactly; floating point within the
+tolerance stated next to each assertion. Inputs with
+integer-valued embeddings make every score exact in fp32, so the top-K tests
+on them are bit-exact including ties (tie-break: score desc, item id asc).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from divrec import ops
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _int_table(rng, n, d, lo=-3, hi=3):
+    return rng.integers(lo, hi + 1, size=(n, d)).astype(np.float32)
+
+
+def _bf16(x):
+    return torch.from_numpy(x).to(DEV).to(torch.bfloat16)
+
+
+# --------------------------------------------------------------------------- gather_dot
+@pytest.mark.parametrize("d", [32, 64, 96, 128, 256])
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_gather_dot(d, dtype):
+    rng = np.random.default_rng(d)
+    U = rng.standard_normal((300, d)).astype(np.float32)
+    I = rng.standard_normal((500, d)).astype(np.float32)
+    if dtype == "bf16":
+        U, I = oracle.as_bf16_f32(U), oracle.as_bf16_f32(I)
+    n = 5003
+    uid = rng.integers(0, 300, n)
+    iid = rng.integers(0, 500, n)
+    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+    got = ops.gather_dot(
+        torch.from_numpy(U).to(DEV).to(tdt), torch.from_numpy(I).to(DEV).to(tdt),
+        torch.from_numpy(uid).to(DEV), torch.from_numpy(iid).to(DEV),
+    ).cpu().numpy()
+    ref = oracle.mf_forward(U, I, uid, iid)
+    # tolerance: fp32 sum-order difference, |err| <= 4e-7 * d * max|u*i|
+    scale = np.abs(U[uid] * I[iid]).max(axis=1) * d
+    assert np.all(np.abs(got - ref) <= 4e-7 * scale + 1e-6)
+
+
+def test_gather_dot_integer_exact():
+    rng = np.random.default_rng(7)
+    U, I = _int_table(rng, 50, 128), _int_table(rng, 70, 128)
+    uid, iid = rng.integers(0, 50, 999), rng.integers(0, 70, 999)
+    got = ops.gather_dot(torch.from_numpy(U).to(DEV), torch.from_numpy(I).to(DEV),
+                         torch.from_numpy(uid).to(DEV), torch.from_numpy(iid).to(DEV))
+    assert np.array_equal(got.cpu().numpy(), oracle.mf_forward(U, I, uid, iid))
+
+
+def test_gather_dot_backward():
+    rng = np.random.default_rng(3)
+    d = 64
+    U = rng.standard_normal((40, d)).astype(np.float32)
+    I = rng.standard_normal((60, d)).astype(np.float32)
+    uid, iid = rng.integers(0, 40, 2000), rng.integers(0, 60, 2000)
+    go = rng.standard_normal(2000).astype(np.float32)
+    gU = torch.zeros(40, d, device=DEV)
+    gI = torch.zeros(60, d, device=DEV)
+    ops.gather_dot_backward(torch.from_numpy(U).to(DEV), torch.from_numpy(I).to(DEV),
+                            torch.from_numpy(uid).to(DEV), torch.from_numpy(iid).to(DEV),
+                            torch.from_numpy(go).to(DEV), gU, gI)
+    rU = np.zeros((40, d)); np.add.at(rU, uid, go[:, None].astype(np.float64) * I[iid])
+    rI = np.zeros((60, d)); np.add.at(rI, iid, go[:, None].astype(np.float64) * U[uid])
+    assert np.allclose(gU.cpu().numpy(), rU, rtol=1e-4, atol=1e-4)
+    assert np.allclose(gI.cpu().numpy(), rI, rtol=1e-4, atol=1e-4)
+
+
+# --------------------------------------------------------------------------- score_topk
+@pytest.mark.parametrize("d", [32, 64, 128, 256])
+@pytest.mark.parametrize("k", [1, 10, 100])
+def test_score_topk_integer_exact(d, k):
+    rng = np.random.default_rng(1000 * d + k)
+    nu, ni = 37 + d, 2000 + 13  # partial user block, partial item tile
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    s, it = ops.score_topk(_bf16(U), _bf16(I), k)
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, return_scores=True)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy(), ref_s)
+
+
+def test_score_topk_ties_exact():
+    # values in {-1, 0, 1} at d=32: massive ties; order must be score desc, id asc
+    rng = np.random.default_rng(11)
+    U, I = _int_table(rng, 70, 32, -1, 1), _int_table(rng, 3000, 32, -1, 1)
+    s, it = ops.score_topk(_bf16(U), _bf16(I), 100)
+    ref_i = oracle.recommend_topk(U, I, 100)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+
+
+def test_score_topk_user_ids_and_item_base():
+    rng = np.random.default_rng(5)
+    U, I = _int_table(rng, 300, 64), _int_table(rng, 4000, 64)
+    users = np.array([299, 0, 17, 17, 150], dtype=np.int64)
+    s, it = ops.score_topk(_bf16(U), _bf16(I), 20, user_ids=torch.from_numpy(users).to(DEV),
+                           item_base=1_000_000)
+    ref_i = oracle.recommend_topk(U, I, 20, users=users)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64) - 1_000_000, ref_i)
+
+
+def test_score_topk_exclusion_exact():
+    rng = np.random.default_rng(9)
+    nu, ni, d, k = 130, 3000, 64, 50
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    frozen = [rng.choice(ni, size=rng.integers(0, 400), replace=False) for _ in range(nu)]
+    # make some excluded items the best ones (worst case for the threshold)
+    for u in range(0, nu, 3):
+        best = np.argsort(-(I @ U[u]), kind="stable")[:30]
+        frozen[u] = np.union1d(frozen[u], best)
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    s, it = ops.score_topk(_bf16(U), _bf16(I), k,
+                           exclude=(torch.from_numpy(rowptr).to(DEV), torch.from_numpy(cols).to(DEV)))
+    ref_i = oracle.recommend_topk(U, I, k, frozen=frozen)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+
+
+def test_score_topk_chunked_catalog_exact():
+    # large catalog, few users: the planner splits items into chunks and merges
+    rng = np.random.default_rng(21)
+    U, I = _int_table(rng, 40, 32), _int_table(rng, 300_001, 32)
+    s, it = ops.score_topk(_bf16(U), _bf16(I), 100)
+    ref_i, ref_s = oracle.recommend_topk(U, I, 100, return_scores=True)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy(), ref_s)
+
+
+def test_score_topk_float_tolerance():
+    rng = np.random.default_rng(2)
+    d, k = 128, 100
+    U = oracle.as_bf16_f32(rng.standard_normal((200, d)).astype(np.float32) / np.sqrt(d))
+    I = oracle.as_bf16_f32(rng.standard_normal((20000, d)).astype(np.float32) / np.sqrt(d))
+    s, it = ops.score_topk(_bf16(U), _bf16(I), k)
+    s, it = s.cpu().numpy(), it.cpu().numpy().astype(np.int64)
+    S = U.astype(np.float64) @ I.astype(np.float64).T
+    tol = 1e-5 * np.sqrt(d / 64)  # |score error| bound vs float64 (scores are O(1))
+    got_true = np.take_along_axis(S, it, axis=1)
+    assert np.all(np.abs(s - got_true) <= tol)
+    assert np.all(np.diff(s, axis=1) <= 0)
+    kth = -np.sort(-S, axis=1)[:, k - 1]
+    # every returned item is within tol of the true top-k; every item clearly
+    # inside the true top-k (margin > 2 tol) is returned
+    assert np.all(got_true >= kth[:, None] - 2 * tol)
+    for u in range(S.shape[0]):
+        must = np.nonzero(S[u] > kth[u] + 2 * tol)[0]
+        assert np.isin(must, it[u]).all()
+
+
+def test_topk_merge_matches_oracle():
+    rng = np.random.default_rng(4)
+    P, n, k = 4, 33, 25
+    sc = rng.integers(-5, 5, size=(P, n, k)).astype(np.float32)
+    sc = -np.sort(-sc, axis=2)
+    items = np.stack([rng.permutation(10000)[: n * k].reshape(n, k) for _ in range(P)]).astype(np.int32)
+    # sort each list by (score desc, item asc) so inputs are valid partials
+    for p in range(P):
+        for u in range(n):
+            o = np.lexsort((items[p, u], -sc[p, u]))
+            sc[p, u], items[p, u] = sc[p, u][o], items[p, u][o]
+    items[1, 3, 20:] = -1  # empty slots
+    ms, mi = ops.topk_merge(torch.from_numpy(sc).to(DEV), torch.from_numpy(items).to(DEV), 40)
+    rs, ri = oracle.topk_merge(sc, items, 40)
+    assert np.array_equal(mi.cpu().numpy().astype(np.int64), ri)
+    assert np.array_equal(ms.cpu().numpy(), rs)
+
+
+# --------------------------------------------------------------------------- ILD
+@pytest.mark.parametrize("k", [1, 2, 10, 100])
+def test_ild_dense_f32_bit_exact(k):
+    rng = np.random.default_rng(k)
+    ni = 500
+    D = rng.random((ni, ni)).astype(np.float32)
+    recs = rng.integers(0, ni, size=(64, k))
+    recs[0, :] = recs[0, 0]  # duplicates (diagonal included)
+    got = ops.ild_dense(torch.from_numpy(recs).to(DEV), torch.from_numpy(D).to(DEV)).cpu().numpy()
+    ref = oracle.ild_sequential(recs, D)
+    assert np.array_equal(got, ref, equal_nan=True)
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.int64])
+def test_ild_dense_int_exact(dt):
+    rng = np.random.default_rng(1)
+    D = rng.integers(0, 3, size=(300, 300)).astype(dt)
+    recs = rng.integers(0, 300, size=(50, 10)).astype(np.int32)
+    got = ops.ild_dense(torch.from_numpy(recs).to(DEV), torch.from_numpy(D).to(DEV)).cpu().numpy()
+    assert np.array_equal(got, oracle.ild_sequential(recs, D))
+
+
+def test_ild_labels_exact():
+    rng = np.random.default_rng(8)
+    labels = rng.integers(0, 4, size=5000)
+    recs = rng.integers(0, 5000, size=(300, 100))
+    got = ops.ild_labels(torch.from_numpy(recs).to(DEV), torch.from_numpy(labels).to(DEV)).cpu().numpy()
+    assert np.array_equal(got, oracle.ild_labels(recs, labels))
+    # and the literal reference algorithm on the dense int matrix (20 users)
+    D = (labels[:, None] == labels[None, :]).astype(np.int32)
+    assert np.array_equal(got[:20], oracle.ild_sequential(recs[:20], D))
+
+
+@pytest.mark.parametrize("d", [32, 64, 128, 256])
+@pytest.mark.parametrize("k", [2, 10, 100, 128])
+@pytest.mark.parametrize("kind", ["cosine", "dot", "euclidean"])
+def test_ild_embedding(d, k, kind):
+    rng = np.random.default_rng(d + k)
+    E = oracle.as_bf16_f32(rng.standard_normal((3000, d)).astype(np.float32))
+    recs = rng.integers(0, 3000, size=(40, k))
+    got = ops.ild_embedding(torch.from_numpy(recs).to(DEV), _bf16(E), kind).cpu().numpy()
+    ref = oracle.ild_embedding_f64(recs, E, kind)
+    # fp32 Gram + fp32 pair sum vs float64: rel 2e-5 (k <= 128)
+    assert np.allclose(got, ref, rtol=2e-5, atol=2e-5 * np.abs(ref).max())
+
+
+# --------------------------------------------------------------------------- BPR + Adam
+def test_bpr_fwd_bwd():
+    rng = np.random.default_rng(6)
+    d, nu, ni, B = 128, 200, 300, 4096
+    U = rng.standard_normal((nu, d)).astype(np.float32) * 0.3
+    I = rng.standard_normal((ni, d)).astype(np.float32) * 0.3
+    uid, pid, nid = rng.integers(0, nu, B), rng.integers(0, ni, B), rng.integers(0, ni, B)
+    gU = torch.zeros(nu, d, device=DEV)
+    gI = torch.zeros(ni, d, device=DEV)
+    loss, hit = ops.bpr_fwd_bwd(torch.from_numpy(U).to(DEV), torch.from_numpy(I).to(DEV),
+                                torch.from_numpy(uid).to(DEV), torch.from_numpy(pid).to(DEV),
+                                torch.from_numpy(nid).to(DEV), 1.0 / B, gU, gI)
+    rl, ra, rU, rI = oracle.bpr_forward_backward(U, I, uid, pid, nid)
+    assert abs(loss.double().mean().item() - rl) <= 1e-5 * abs(rl)
+    assert abs(hit.double().mean().item() - ra) <= 1.0 / B
+    assert np.allclose(gU.cpu().numpy(), rU, rtol=1e-4, atol=1e-7)
+    assert np.allclose(gI.cpu().numpy(), rI, rtol=1e-4, atol=1e-7)
+
+
+def test_adam_dense_matches_torch():
+    rng = np.random.default_rng(12)
+    p0 = rng.standard_normal(10007).astype(np.float32)
+    grads = [rng.standard_normal(10007).astype(np.float32) for _ in range(3)]
+    # torch reference on the same device
+    pt = torch.nn.Parameter(torch.from_numpy(p0.copy()).to(DEV))
+    opt = torch.optim.Adam([pt], lr=1e-3, foreach=False)
+    p = torch.from_numpy(p0.copy()).to(DEV)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    for step, g in enumerate(grads, 1):
+        pt.grad = torch.from_numpy(g).to(DEV)
+        opt.step()
+        ops.adam_dense(p, torch.from_numpy(g).to(DEV), m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, step)
+    assert torch.allclose(p, pt.detach(), rtol=0, atol=1e-6)
+
+
+# --------------------------------------------------------------------------- MMR
+@pytest.mark.parametrize("lam", [1.0, 0.7, 0.3])
+def test_mmr_rerank(lam):
+    rng = np.random.default_rng(int(lam * 10))
+    d, ni, n, C, kout = 128, 5000, 8, 300, 40
+    E = oracle.as_bf16_f32(rng.standard_normal((ni, d)).astype(np.float32))
+    cand = np.stack([rng.choice(ni, C, replace=False) for _ in range(n)]).astype(np.int32)
+    sc = rng.standard_normal((n, C)).astype(np.float32)
+    got = ops.mmr_rerank(torch.from_numpy(cand).to(DEV), torch.from_numpy(sc).to(DEV), _bf16(E),
+                         kout, lam).cpu().numpy()
+    assert oracle.mmr_check(got, cand, sc, E, lam, tol=1e-4) == 0
+    if lam == 1.0:  # pure relevance: equals top-k by score (ties: lowest position)
+        ref = np.take_along_axis(cand, np.argsort(-sc, axis=1, kind="stable")[:, :kout], axis=1)
+        assert np.array_equal(got, ref)
