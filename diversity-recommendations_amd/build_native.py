@@ -40,11 +40,11 @@ def _headers_mtime() -> float:
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
-def _compile(src: Path, verbose: bool) -> Path:
-    obj = OBJ_DIR / (src.stem + ".o")
+def _compile(src: Path, verbose: bool, obj_dir: Path = OBJ_DIR, extra=()) -> Path:
+    obj = obj_dir / (src.stem + ".o")
     if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
         return obj
-    cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *extra, "-c", str(src), "-o", str(obj)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -53,32 +53,39 @@ def _compile(src: Path, verbose: bool) -> Path:
     return obj
 
 
-def build(jobs: int = 4, verbose: bool = False) -> Path:
-    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+def build(jobs: int = 4, verbose: bool = False, diag: bool = False) -> Path:
+    """Build the product library, or with diag=True the instrumented
+    libdivrec_hip_diag.so (-DDR_TOPK_DIAG; profiling only, never loaded by
+    the product path unless DIVREC_HIP_LIB points at it)."""
+    obj_dir = OBJ_DIR.parent / "obj_diag" if diag else OBJ_DIR
+    lib_path = LIB_DIR / "libdivrec_hip_diag.so" if diag else LIB_PATH
+    extra = ("-DDR_TOPK_DIAG",) if diag else ()
+    obj_dir.mkdir(parents=True, exist_ok=True)
     LIB_DIR.mkdir(parents=True, exist_ok=True)
     srcs = sorted(CSRC.glob("*.hip"))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
+        objs = list(ex.map(lambda s: _compile(s, verbose, obj_dir, extra), srcs))
     newest = max(o.stat().st_mtime for o in objs)
-    if LIB_PATH.exists() and LIB_PATH.stat().st_mtime >= newest:
-        return LIB_PATH
-    tmp = LIB_PATH.with_suffix(".so.tmp")
+    if lib_path.exists() and lib_path.stat().st_mtime >= newest:
+        return lib_path
+    tmp = lib_path.with_suffix(".so.tmp")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, lib_path)
+    return lib_path
 
 
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--diag", action="store_true", help="build the instrumented diag library")
     args = ap.parse_args()
-    path = build(args.jobs, args.verbose)
+    path = build(args.jobs, args.verbose, args.diag)
     print(path)
     return 0
 

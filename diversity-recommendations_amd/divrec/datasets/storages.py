@@ -1,0 +1,113 @@
+"""Interaction / feature containers (host side).
+
+Mirrors reference divrec/datasets/storages.py:7-110: the same dataclass
+fields, derived counts and validation asserts. These are plain host data
+structures (the index streams the GPU kernels consume); nothing here computes
+on the hot path. Divergence (documented in INTEGRATION.md): derived
+``number_of_users`` / ``number_of_items`` are Python ints, where the reference
+leaves a 0-d tensor when it derives them from the data (storages.py:63-64).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+import torch
+
+
+@dataclass
+class Features:
+    """Table with named columns (reference storages.py:7-30)."""
+
+    features: torch.Tensor = None
+    feature_names: List[str] = field(default_factory=list)
+    number_of_features: int = 0
+
+    def __post_init__(self):
+        self.number_of_features = max(self.number_of_features, self.features.size(1))
+        assert len(self.feature_names) == self.number_of_features
+
+    def __len__(self) -> int:
+        return self.features.size(0)
+
+    def __getitem__(self, name: str) -> torch.Tensor:
+        return self.features[:, self.feature_names.index(name)]
+
+    def __contains__(self, name: str) -> bool:
+        return name in self.feature_names
+
+
+@dataclass
+class UserItemInteractionsDataset:
+    """User-item interactions with optional scores and features
+    (reference storages.py:33-94)."""
+
+    interactions: Optional[torch.LongTensor] = None
+    interaction_scores: Optional[torch.Tensor] = None
+    user_features: Optional[Features] = None
+    item_features: Optional[Features] = None
+
+    number_of_interactions: int = 0
+    number_of_users: int = 0
+    number_of_items: int = 0
+
+    def __post_init__(self):
+        if self.interactions is not None:
+            n, cols = self.interactions.size()
+            self.number_of_interactions = n
+            assert cols == 2
+            if self.interaction_scores is None:
+                self.interaction_scores = torch.ones(n)
+            assert self.interaction_scores.size(0) == n
+            users = torch.unique(self.interactions[:, 0])
+            items = torch.unique(self.interactions[:, 1])
+            self.number_of_users = max(int(self.number_of_users), int(users.max()) + 1)
+            self.number_of_items = max(int(self.number_of_items), int(items.max()) + 1)
+            assert bool(torch.all((users >= 0) & (users < self.number_of_users)))
+            assert bool(torch.all((items >= 0) & (items < self.number_of_items)))
+        if self.interaction_scores is not None:
+            assert self.interactions is not None
+            assert self.interaction_scores.size(0) == self.number_of_interactions
+        if self.user_features is not None:
+            if self.number_of_users == 0:
+                self.number_of_users = len(self.user_features)
+            assert self.number_of_users == len(self.user_features)
+        if self.item_features is not None:
+            if self.number_of_items == 0:
+                self.number_of_items = len(self.item_features)
+            assert self.number_of_items == len(self.item_features)
+
+    def has_interactions(self) -> bool:
+        return self.interactions is not None
+
+    def has_user_features(self) -> bool:
+        return self.user_features is not None
+
+    def has_item_features(self) -> bool:
+        return self.item_features is not None
+
+    def user_item_csr(self, n_users: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Per-user sorted, de-duplicated item ids as CSR (rowptr int64
+        [n_users+1], items int32): the exclusion lists / positives the GPU
+        kernels consume in place of the reference's per-user Python set ops."""
+        n_users = self.number_of_users if n_users is None else n_users
+        if self.interactions is None or self.interactions.numel() == 0:
+            return torch.zeros(n_users + 1, dtype=torch.int64), torch.zeros(0, dtype=torch.int32)
+        inter = torch.unique(self.interactions.to(torch.int64), dim=0)  # sorted by (user, item)
+        inter = inter[inter[:, 0] < n_users]
+        counts = torch.bincount(inter[:, 0], minlength=n_users)
+        rowptr = torch.zeros(n_users + 1, dtype=torch.int64)
+        rowptr[1:] = torch.cumsum(counts, 0)
+        return rowptr, inter[:, 1].to(torch.int32).contiguous()
+
+
+def get_user_features(data: UserItemInteractionsDataset, user_id: int) -> Optional[torch.Tensor]:
+    if data.user_features is None:
+        return None
+    return data.user_features.features[user_id]
+
+
+def get_item_features(data: UserItemInteractionsDataset, item_id: int) -> Optional[torch.Tensor]:
+    if data.item_features is None:
+        return None
+    return data.item_features.features[item_id]

@@ -1,0 +1,26 @@
+"""Entropy diversity of the recommended items (reference
+divrec/metrics/entropy_diversity_score.py:8-26): normalised Shannon entropy of
+the recommendation histogram between log(k) and log(#items). Catalog-level
+statistic (SURVEY.md §8f rank 2, next tier): tensor ops on the device."""
+import math
+
+import torch
+
+from divrec.losses.base_losses import DatasetAwareLoss, RecommendationsAwareLoss
+
+
+class EntropyDiversityScore(RecommendationsAwareLoss, DatasetAwareLoss):
+    def __init__(self, *args, **kwargs):
+        DatasetAwareLoss.__init__(self, *args, **kwargs)
+        RecommendationsAwareLoss.__init__(self, *args, **kwargs)
+        self.max_entropy = math.log(self.dataset.number_of_items)
+
+    def forward(self, interactions, recommendations):
+        return self.recommendations_loss(interactions, recommendations)
+
+    def recommendations_loss(self, interactions, recommendations) -> torch.Tensor:
+        _, counts = torch.unique(recommendations, return_counts=True)
+        p = counts / counts.sum()
+        actual = -torch.sum(p * torch.log(p))
+        min_entropy = math.log(recommendations.size(1))
+        return (actual - min_entropy) / (self.max_entropy - min_entropy)

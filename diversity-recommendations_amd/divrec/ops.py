@@ -304,3 +304,26 @@ def mmr_rerank(
     )
     B.check(rc, "dr_mmr_rerank")
     return out
+
+
+# --------------------------------------------------------------------------- rank metrics
+def rank_metrics(
+    recs: torch.Tensor, pos_rowptr: torch.Tensor, pos_items: torch.Tensor
+) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """(precision@k, recall@k, AP@k, NDCG@k) per user of ``recs`` [n, k] against
+    positives given as CSR (rowptr int64 [n+1], items int32 sorted per row)."""
+    dev = B.require_device(recs, pos_rowptr, pos_items)
+    recs, rc_dt = _recs(recs)
+    n, k = recs.shape
+    _need(pos_rowptr.dtype == torch.int64 and pos_rowptr.numel() == n + 1, "rowptr int64 [n+1]")
+    _need(pos_items.dtype == torch.int32, "positives must be int32")
+    outs = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(4)]
+    if n == 0:
+        return tuple(outs)
+    items = pos_items.contiguous() if pos_items.numel() else torch.zeros(1, dtype=torch.int32, device=dev)
+    rc = B.lib().dr_rank_metrics(
+        recs.data_ptr(), rc_dt, n, k, pos_rowptr.contiguous().data_ptr(), items.data_ptr(),
+        *(o.data_ptr() for o in outs), B.stream(dev),
+    )
+    B.check(rc, "dr_rank_metrics")
+    return tuple(outs)

@@ -1,0 +1,243 @@
+"""Training / scoring loops (reference divrec/train/utils.py:10-216).
+
+Same functions, arguments and return values as the reference. On the hot path:
+
+* ``get_model_recommendations`` with a MatrixFactorization model runs ONE
+  dr_score_topk over all users (bf16 MFMA scores, fused top-k, frozen items
+  excluded through a CSR) instead of the reference's per-user loop of set
+  differences, full-catalog forward and full argsort (:58-77). Ties are broken
+  by item id ascending (the reference's argsort is unstable there, :73).
+* ``pair_wise_train_loop`` with MatrixFactorization + LogSigmoidDifferenceLoss
+  runs each batch as ONE dr_bpr_fwd_bwd (gather, loss, AUC flags and dense
+  embedding gradients fused) followed by dr_adam_dense when the optimizer is a
+  plain torch.optim.Adam (its state tensors are used and kept up to date, so
+  the optimizer stays usable). Other combinations take the generic path: the
+  model's HIP forward/backward under autograd and ``optimizer.step()``.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+
+from divrec import ops
+from divrec.datasets import PairWiseDataset, PointWiseDataset, RankingDataset
+from divrec.losses import (
+    LogSigmoidDifferenceLoss,
+    PairWiseLoss,
+    PointWiseLoss,
+    RecommendationsAwareLoss,
+)
+from divrec.metrics import AUCScore
+from divrec.models import MatrixFactorization, RankingModel
+
+
+def _model_device(model: torch.nn.Module) -> Optional[torch.device]:
+    for p in model.parameters():
+        return p.device
+    return None
+
+
+def _to(t, device):
+    return t.to(device, non_blocking=True) if isinstance(t, torch.Tensor) and device else t
+
+
+# --------------------------------------------------------------------------- scoring
+def point_wise_score_loop(dataset: PointWiseDataset, model: RankingModel,
+                          losses: List[PointWiseLoss], **loader_params):
+    model.eval()
+    dev = _model_device(model)
+    values = {loss.__class__.__name__: [] for loss in losses}
+    with torch.no_grad():
+        for user_id, item_id, uf, itf, true_rel in dataset.loader(**loader_params):
+            pred = model(user_id, item_id, uf, itf)
+            for loss in losses:
+                values[loss.__class__.__name__].append(loss.point_wise(_to(true_rel, pred.device), pred))
+    return [loss.reduce_loss_values(torch.concatenate(values[loss.__class__.__name__]))
+            for loss in losses]
+
+
+def pair_wise_score_loop(dataset: PairWiseDataset, model: RankingModel,
+                         losses: List[PairWiseLoss], **loader_params):
+    model.eval()
+    values = {loss.__class__.__name__: [] for loss in losses}
+    with torch.no_grad():
+        for user_id, pos, neg, uf, pf, nf in dataset.loader(**loader_params):
+            positives = model(user_id, pos, uf, pf)
+            negatives = model(user_id, neg, uf, nf)
+            for loss in losses:
+                values[loss.__class__.__name__].append(loss.pair_wise(positives, negatives))
+    return [loss.reduce_loss_values(torch.concatenate(values[loss.__class__.__name__]))
+            for loss in losses]
+
+
+def get_model_recommendations(dataset: RankingDataset, model: RankingModel,
+                              number_of_recommendations: int) -> torch.LongTensor:
+    """Top-``number_of_recommendations`` candidates of every user of
+    ``dataset`` (LongTensor [U, k] on the CPU, like the reference)."""
+    k = int(number_of_recommendations)
+    n_users = int(dataset.data.number_of_users)
+    if isinstance(model, MatrixFactorization):
+        user_ids = None if n_users == model.no_users else torch.arange(n_users)
+        excl = dataset.exclusion_csr()
+        items, _ = model.score_topk(k, user_ids=user_ids, exclude=excl)
+        return items.cpu()
+    # Generic RankingModel: the reference loop (model scores per user), with
+    # the deterministic tie-break. Outside the MF hot path.
+    recs = []
+    with torch.no_grad():
+        for rep_user, _, cands, uf, itf in dataset:
+            scores = model(rep_user, cands, uf, itf).to("cpu")
+            order = torch.sort(scores, descending=True, stable=True).indices
+            recs.append(cands[order][:k].tolist())
+    return torch.LongTensor(recs)
+
+
+def recommendations_score_loop(dataset: RankingDataset, model: RankingModel,
+                               losses: List[RecommendationsAwareLoss],
+                               number_of_recommendations: int):
+    model.eval()
+    interactions = dataset.data.interactions
+    recommendations = get_model_recommendations(dataset, model, number_of_recommendations)
+    return [loss(interactions, recommendations) for loss in losses]
+
+
+# --------------------------------------------------------------------------- training
+def point_wise_train_loop(dataset: PointWiseDataset, model: RankingModel, loss: PointWiseLoss,
+                          optimizer: torch.optim.Optimizer,
+                          scores: Optional[List[PointWiseLoss]] = None,
+                          **loader_params) -> Tuple[float, List[float]]:
+    assert scores is None or all(score.reduce for score in scores)
+    model.train()
+    batch_count, mean_loss = 0, 0.0
+    mean_scores = [0.0] * (len(scores) if scores is not None else 0)
+    for user_id, item_id, uf, itf, true_rel in dataset.loader(**loader_params):
+        pred = model(user_id, item_id, uf, itf)
+        true_rel = _to(true_rel, pred.device)
+        loss_value = loss(true_rel, pred)
+        loss_value.backward()
+        optimizer.step()
+        optimizer.zero_grad()
+        batch_count += 1
+        mean_loss += loss_value.item()
+        if scores is not None:
+            for i, score in enumerate(scores):
+                mean_scores[i] += score(true_rel, pred).item()
+    return mean_loss / batch_count, [s / batch_count for s in mean_scores]
+
+
+def _plain_adam(optimizer: torch.optim.Optimizer) -> bool:
+    if type(optimizer) is not torch.optim.Adam:
+        return False
+    for g in optimizer.param_groups:
+        if g.get("amsgrad") or g.get("maximize") or g.get("capturable") or g.get("differentiable"):
+            return False
+        if g.get("decoupled_weight_decay", False):
+            return False
+    return True
+
+
+def fused_adam_step(optimizer: torch.optim.Adam) -> None:
+    """optimizer.step() of a plain torch.optim.Adam done by dr_adam_dense, on
+    the optimizer's own state (step / exp_avg / exp_avg_sq), so torch's
+    optimizer remains consistent and resumable."""
+    for group in optimizer.param_groups:
+        beta1, beta2 = group["betas"]
+        for p in group["params"]:
+            if p.grad is None:
+                continue
+            st = optimizer.state[p]
+            if len(st) == 0:
+                st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["step"] += 1
+            ops.adam_dense(p.data, p.grad, st["exp_avg"], st["exp_avg_sq"], group["lr"], beta1,
+                           beta2, group["eps"], group["weight_decay"], int(st["step"].item()))
+
+
+def _bpr_fast_path(model, loss, scores) -> bool:
+    return (isinstance(model, MatrixFactorization) and type(loss) is LogSigmoidDifferenceLoss
+            and (scores is None or all(type(s) is AUCScore for s in scores)))
+
+
+def pair_wise_train_loop(dataset: PairWiseDataset, model: RankingModel, loss: PairWiseLoss,
+                         optimizer: torch.optim.Optimizer,
+                         scores: Optional[List[PairWiseLoss]] = None,
+                         **loader_params) -> Tuple[float, List[float]]:
+    """One epoch of pairwise training; returns (mean batch loss, [mean score])."""
+    assert scores is None or all(score.reduce for score in scores)
+    model.train()
+    n_scores = len(scores) if scores is not None else 0
+    batch_losses, batch_scores = [], []
+    fused = _bpr_fast_path(model, loss, scores)
+    adam = _plain_adam(optimizer)
+    for user_id, pos, neg, uf, pf, nf in dataset.loader(**loader_params):
+        if fused:
+            dev = model._device()
+            U, I = model.user_embeddings.weight, model.item_embeddings.weight
+            uid, pid, nid = (t.to(dev, torch.int64, non_blocking=True) for t in (user_id, pos, neg))
+            if U.grad is None:
+                U.grad = torch.zeros_like(U)
+            if I.grad is None:
+                I.grad = torch.zeros_like(I)
+            B = uid.numel()
+            losses_b, hits = ops.bpr_fwd_bwd(U.data, I.data, uid, pid, nid, 1.0 / B, U.grad, I.grad)
+            loss_value = torch.sum(losses_b, dim=0) / B
+            if adam:
+                fused_adam_step(optimizer)
+            else:
+                optimizer.step()
+            optimizer.zero_grad()
+            batch_losses.append(loss_value.detach())
+            if n_scores:
+                auc = torch.sum(hits.float(), dim=0) / B
+                batch_scores.append(torch.stack([auc] * n_scores))
+        else:
+            positives = model(user_id, pos, uf, pf)
+            negatives = model(user_id, neg, uf, nf)
+            loss_value = loss(positives, negatives)
+            loss_value.backward()
+            optimizer.step()
+            optimizer.zero_grad()
+            batch_losses.append(loss_value.detach())
+            if n_scores:
+                batch_scores.append(torch.stack(
+                    [s(positives.detach(), negatives.detach()).float() for s in scores]))
+    count = len(batch_losses)
+    # per-batch values summed as Python floats in batch order, like the reference
+    mean_loss = sum(float(v) for v in torch.stack(batch_losses).double().cpu().tolist()) / count
+    means = [0.0] * n_scores
+    if n_scores:
+        rows = torch.stack(batch_scores).double().cpu().tolist()
+        means = [sum(r[i] for r in rows) / count for i in range(n_scores)]
+    return mean_loss, means
+
+
+def recommendations_train_loop(dataset: RankingDataset, model: RankingModel,
+                               loss: RecommendationsAwareLoss, number_of_recommendations: int,
+                               optimizer: torch.optim.Optimizer,
+                               scores: Optional[List[RecommendationsAwareLoss]] = None
+                               ) -> Tuple[float, List[float]]:
+    """The reference's listwise loop (:167-216), kept for API completeness: it
+    ranks ASCENDING and back-propagates through integer recommendations, so
+    with the shipped losses it fails at backward() exactly as the reference."""
+    assert scores is None or all(score.reduce for score in scores)
+    model.train()
+    batch_count, mean_loss = 0, 0.0
+    mean_scores = [0.0] * (len(scores) if scores is not None else 0)
+    for rep_user, _, cands, uf, itf in dataset:
+        model_scores = model(rep_user, cands, uf, itf)
+        inter = dataset.data.interactions
+        interactions = inter[inter[:, 0] == rep_user[0]]
+        recommendations = cands[torch.argsort(model_scores.cpu())][:number_of_recommendations]
+        loss_value = loss(interactions, recommendations)
+        loss_value.backward()
+        optimizer.step()
+        optimizer.zero_grad()
+        batch_count += 1
+        mean_loss += loss_value.item()
+        if scores is not None:
+            for i, score in enumerate(scores):
+                mean_scores[i] += score(interactions, recommendations).item()
+    return mean_loss / batch_count, [s / batch_count for s in mean_scores]

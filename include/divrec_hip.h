@@ -158,6 +158,18 @@ int dr_adam_dense(float* param, const float* grad, float* exp_avg, float* exp_av
                   double weight_decay, int64_t step, dr_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Accuracy metrics of top-k lists against test interactions, per user
+ * (SURVEY.md §8f rank 1): precision@k (divrec/metrics/precision_at_k.py:6-22),
+ * recall@k (recall_at_k.py:6-22), AP@k with the reference's formula
+ * sum_p cumhits(p)/(p+1) / k (average_precision_at_k.py:6-24) and NDCG@k
+ * (normalized_discounted_cumulative_gain.py:6-23). Positives as CSR: rowptr
+ * int64 [n_users+1], items int32 sorted per row. Any output may be NULL.
+ * recall is NaN for a user without positives (the reference divides by 0). */
+int dr_rank_metrics(const void* recs, int rec_dtype, int64_t n_users, int k,
+                    const int64_t* pos_rowptr, const int32_t* pos_items, float* precision,
+                    float* recall, float* avg_precision, float* ndcg, dr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * MMR diversity re-rank (config 5; no reference symbol — SURVEY.md §8a a16):
  * per user, greedily pick k_out of the C candidates maximising
  *   lambda * score_i - (1 - lambda) * max_{j in S} cos(e_i, e_j)

@@ -76,16 +76,26 @@ def recommend_topk(
     users: Optional[Sequence[int]] = None,
     frozen: Optional[List[Sequence[int]]] = None,
     return_scores: bool = False,
+    block: int = 1 << 18,
 ):
     """get_model_recommendations (divrec/train/utils.py:53-77) with
     MatrixFactorization scores: per user, score every candidate with
-    sum(u * i) in fp32 and keep candidates[order][:k]."""
+    sum(u * i) in fp32 (products rounded to fp32, summed over d) and keep
+    candidates[order][:k]. Candidates are scored in blocks of ``block`` rows
+    only to bound memory; the arithmetic per (user, item) is unchanged."""
     users = range(U.shape[0]) if users is None else users
     recs, scs = [], []
+    I32 = I if I.dtype == np.float32 else I.astype(np.float32)
     for n, u in enumerate(users):
-        cands = candidates_for_user(I.shape[0], None if frozen is None else frozen[n])
-        s = np.sum(U[u].astype(np.float32)[None, :] * I[cands].astype(np.float32), axis=1,
-                   dtype=np.float32)
+        fz = None if frozen is None else frozen[n]
+        cands = candidates_for_user(I.shape[0], fz)
+        dense = fz is None or len(fz) == 0  # candidates are arange(I): slice, don't gather
+        uu = U[u].astype(np.float32)[None, :]
+        s = np.empty(len(cands), dtype=np.float32)
+        for b0 in range(0, len(cands), block):
+            c = cands[b0 : b0 + block]
+            rows = I32[b0 : b0 + len(c)] if dense else I32[c]
+            s[b0 : b0 + len(c)] = np.sum(uu * rows, axis=1, dtype=np.float32)
         o = topk_order(s, k)
         recs.append(cands[o])
         scs.append(s[o])

@@ -197,6 +197,12 @@ def main():
     mean_loss, (mean_auc,) = train.pair_wise_train_loop(
         pw, mf, losses.LogSigmoidDifferenceLoss(), opt, scores=[metrics.AUCScore()],
         batch_size=64)
+    random.seed(42)
+    triples = []
+    for row in datasets.PairWiseDataset(data, max_sampled=5):
+        triples.append(row[:3])
+    save("pairwise_triples", train=tr, triples=np.asarray(triples, dtype=np.int64),
+         seed=np.int64(42), max_sampled=np.int64(5), n_items=np.int64(40))
     save("bpr_loop", train=tr, U0=U0, I0=I0, U1=mf.user_embeddings.weight,
          I1=mf.item_embeddings.weight, mean_loss=np.float64(mean_loss),
          mean_auc=np.float64(mean_auc), seed=np.int64(42), max_sampled=np.int64(5),
@@ -222,7 +228,19 @@ def main():
     with torch.no_grad():
         res = train.recommendations_score_loop(rds, mf, [ild], 10)
         recs = train.get_model_recommendations(rds, mf, 10)
-    save("ml100k_cfg1", U=U, I=I, train=tr, test=te, recs=recs, ild=res[0])
+    test_inter = te
+    full_ds = datasets.UserItemInteractionsDataset(torch.cat([tr, te]), number_of_users=nu,
+                                                   number_of_items=ni)
+    with torch.no_grad():
+        prec = metrics.precision_at_k(test_inter, recs)
+        rec = metrics.recall_at_k(test_inter, recs)
+        ap = metrics.average_precision_at_k(test_inter, recs)
+        ndcg = metrics.normalized_discounted_cumulative_gain(test_inter, recs)
+        ent = metrics.EntropyDiversityScore(dataset=full_ds)(test_inter, recs)
+        pri = metrics.PRI(dataset=full_ds)(test_inter, recs)
+        mapk = metrics.MeanAveragePrecisionAtKScore()(test_inter, recs)
+    save("ml100k_cfg1", U=U, I=I, train=tr, test=te, recs=recs, ild=res[0], precision=prec,
+         recall=rec, ap=ap, ndcg=ndcg, entropy=ent, pri=pri, map=mapk)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,106 @@
+"""The N>1 path (item-row shards + one all_to_all + merge) on CPU with gloo,
+world_size 2 and 3: the per-rank merged lists must equal the single-process
+top-k over the whole catalog. The local top-k / merge are injected from the
+oracle (CPU checker); the exchange itself is the production code."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from divrec.distributed import exchange_partials, shard_range, sharded_score_topk
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _local_topk(user_table, item_shard, k, user_ids=None, item_base=0):
+    U = user_table.numpy() if user_ids is None else user_table.numpy()[user_ids.numpy()]
+    items, scores = oracle.recommend_topk(U, item_shard.numpy(), k, return_scores=True)
+    return torch.from_numpy(scores.astype(np.float32)), torch.from_numpy((items + item_base).astype(np.int32))
+
+
+def _merge(ps, pi, k):
+    s, i = oracle.topk_merge(ps.numpy(), pi.numpy(), k)
+    return torch.from_numpy(s), torch.from_numpy(i.astype(np.int32))
+
+
+def _worker(rank, world, port, U, I, k, user_ids, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard_range(I.shape[0], world, rank)
+        (s, i), (ulo, uhi) = sharded_score_topk(torch.from_numpy(U), torch.from_numpy(I[lo:hi]), lo, k,
+                                                user_ids=user_ids, local_topk=_local_topk, merge=_merge)
+        q.put((rank, ulo, uhi, s.numpy(), i.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_users,user_ids", [(2, 37, False), (3, 20, True), (2, 1, False)])
+def test_sharded_topk_equals_single_device(world, n_users, user_ids):
+    rng = np.random.default_rng(world * 100 + n_users)
+    U = rng.integers(-3, 4, size=(n_users + 5, 16)).astype(np.float32)   # integer scores: many ties
+    I = rng.integers(-3, 4, size=(1001, 16)).astype(np.float32)
+    k = 25
+    uids = torch.from_numpy(rng.permutation(n_users + 5)[:n_users].astype(np.int64)) if user_ids else None
+    Uq = U[uids.numpy()] if user_ids else U
+    ref_i, ref_s = oracle.recommend_topk(Uq, I, k, return_scores=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, U, I, k, uids, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seen = 0
+    for rank, ulo, uhi, s, i in sorted(got):
+        assert (ulo, uhi) == shard_range(Uq.shape[0], world, rank)
+        assert np.array_equal(i, ref_i[ulo:uhi])
+        assert np.array_equal(s, ref_s[ulo:uhi].astype(np.float32))
+        seen += uhi - ulo
+    assert seen == Uq.shape[0]
+
+
+def _exchange_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, k = 7, 3
+        s = torch.full((n, k), float(rank)) + torch.arange(n, dtype=torch.float32)[:, None] / 10
+        i = torch.full((n, k), rank, dtype=torch.int32) * 1000 + torch.arange(n, dtype=torch.int32)[:, None]
+        ps, pi = exchange_partials(s, i)
+        q.put((rank, ps.numpy(), pi.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_routes_user_slices():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (s, i)) for r, s, i in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        lo, hi = shard_range(7, world, r)
+        s, i = got[r]
+        assert s.shape == (world, hi - lo, 3)
+        for src in range(world):   # row block `src` came from rank src, users lo..hi
+            assert np.array_equal(i[src, :, 0], src * 1000 + np.arange(lo, hi))
+            assert np.allclose(s[src, :, 0], src + np.arange(lo, hi) / 10)

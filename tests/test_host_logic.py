@@ -1,0 +1,95 @@
+"""Host-side logic on CPU: datasets, CSR builders, naming, planner-independent
+API behaviour. No GPU calls."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from divrec.datasets import Features, PairWiseDataset, RankingDataset, UserItemInteractionsDataset
+from divrec.distributed import shard_range
+from divrec.losses import IntraListDiversityScore, LogSigmoidDifferenceLoss
+from divrec.metrics import AUCScore, PrecisionAtKScore
+from divrec.models import MatrixFactorization, RandomModel
+from divrec.utils import to_camel_case
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_metric_names():
+    assert to_camel_case("IntraListDiversityScore") == "intra_list_diversity_score"
+    assert to_camel_case("AUCScore") == "auc_score"
+    assert to_camel_case("PRI") == "pri"
+    assert IntraListDiversityScore(distance_matrix=None).name == "intra_list_diversity_score"
+    assert PrecisionAtKScore().name == "precision_atk_score"  # the reference rule, verbatim
+
+
+def test_interactions_dataset_derivations():
+    inter = torch.LongTensor([[0, 3], [2, 1], [2, 5]])
+    ds = UserItemInteractionsDataset(inter)
+    assert (ds.number_of_users, ds.number_of_items, ds.number_of_interactions) == (3, 6, 3)
+    assert torch.equal(ds.interaction_scores, torch.ones(3))
+    ds2 = UserItemInteractionsDataset(inter, number_of_users=10, number_of_items=4)
+    assert (ds2.number_of_users, ds2.number_of_items) == (10, 6)
+    with pytest.raises(AssertionError):
+        UserItemInteractionsDataset(torch.LongTensor([[0, 1, 2]]))
+    f = Features(torch.zeros(6, 2), ["a", "partition"])
+    assert "partition" in f and len(f) == 6 and f["partition"].shape == (6,)
+
+
+def test_ranking_dataset_candidates_and_csr():
+    rng = np.random.default_rng(0)
+    tr = torch.LongTensor([(u, int(i)) for u in range(5) for i in rng.choice(30, 7, replace=False)])
+    te = torch.LongTensor([(u, int(i)) for u in range(5) for i in rng.choice(30, 2, replace=False)])
+    train = UserItemInteractionsDataset(tr, number_of_users=5, number_of_items=30)
+    test = UserItemInteractionsDataset(te, number_of_users=5, number_of_items=30)
+    rds = RankingDataset(test, frozen=train)
+    rowptr, cols = rds.exclusion_csr()
+    for u, (rep, pos, cands, uf, itf) in enumerate(rds):
+        frozen = tr[tr[:, 0] == u, 1].tolist()
+        assert torch.equal(cands, torch.from_numpy(oracle.candidates_for_user(30, frozen)))
+        assert rep.tolist() == [u] * len(cands)
+        assert sorted(cols[rowptr[u]:rowptr[u + 1]].tolist()) == sorted(set(frozen))
+    # no frozen: every item is a candidate (the reference crashes here)
+    _, _, cands, _, _ = next(iter(RankingDataset(test)))
+    assert torch.equal(cands, torch.arange(30))
+    assert RankingDataset(test).exclusion_csr() is None
+
+
+def test_pairwise_sampling_matches_reference_stream():
+    import random
+
+    g = np.load(os.path.join(GOLD, "pairwise_triples.npz"), allow_pickle=False)
+    tr = torch.from_numpy(g["train"])
+    n_items = int(g["n_items"])
+    data = UserItemInteractionsDataset(tr, user_features=Features(torch.zeros(12, 1), ["x"]),
+                                       item_features=Features(torch.zeros(n_items, 1), ["x"]))
+    random.seed(int(g["seed"]))
+    got = [row[:3] for row in PairWiseDataset(data, max_sampled=int(g["max_sampled"]))]
+    assert np.array_equal(np.asarray(got, dtype=np.int64), g["triples"])
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 7, 10_000_001):
+        for w in (1, 2, 3, 8):
+            parts = [shard_range(n, w, r) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+            assert max(h - l for l, h in parts) - min(h - l for l, h in parts) <= 1
+
+
+def test_models_state_dict_and_cpu_guard():
+    mf = MatrixFactorization(7, 9, 16)
+    assert set(mf.state_dict()) == {"user_embeddings.weight", "item_embeddings.weight"}
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        mf(torch.LongTensor([0]), torch.LongTensor([1]))
+    assert RandomModel(3, 4)(torch.LongTensor([0, 1]), torch.LongTensor([2, 3])).shape == (2,)
+
+
+def test_pairwise_losses_are_elementwise():
+    pos, neg = torch.tensor([1.0, 0.0, -2.0]), torch.tensor([0.0, 0.0, 1.0])
+    loss = LogSigmoidDifferenceLoss(reduction="none")  # ignored, as the reference
+    assert loss.reduction == "mean"
+    assert torch.allclose(loss.pair_wise(pos, neg), -torch.nn.functional.logsigmoid(pos - neg))
+    assert AUCScore(reduction="none")(pos, neg).tolist() == [1, 1, 0]
