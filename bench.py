@@ -212,7 +212,7 @@ def main():
             "unit": "TFLOP/s",
             "frac": achieved / MFMA_BF16_PEAK_TFLOPS,
             "traffic": traffic,
-            "kernel": "score_topk_kernel<128,1024> (+ chunk merge)",
+            "kernel": "dr_score_topk = score_scan_kernel (MFMA scan + fused threshold top-k) + topk_finalize_kernel; timed together",
             "flop_per_launch": flops,
         },
         "cpu_baseline": None,

@@ -1,0 +1,263 @@
+"""Drop-in API on the GPU against the golden vectors the REFERENCE produced
+(tests/golden/make_golden.py). Every call goes through the divrec package ->
+ctypes -> libdivrec_hip.so. Tolerances:
+  * indices: exact on integer-valued tables; on float tables exact wherever
+    the reference's neighbouring scores are separated by more than the score
+    tolerance (bf16 products are exact in fp32, only the summation order
+    differs: |ds| <= 1e-5 * sqrt(d/64) for O(1) scores);
+  * ILD from a dense D: bit-exact (same fp32 accumulation order);
+  * accuracy metrics on identical lists: rel 1e-6;
+  * BPR loss rel 1e-6, grads rel 1e-5 (fp32 atomics reorder the sums).
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from divrec import datasets, losses, metrics, models, ops, train
+from divrec.losses import EmbeddingDistance, LabelEquality
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+DEV = torch.device("cuda", 0)
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, f"{name}.npz"), allow_pickle=False)
+
+
+def mf_from(U, I, device=DEV):
+    mf = models.MatrixFactorization(U.shape[0], I.shape[0], U.shape[1])
+    with torch.no_grad():
+        mf.user_embeddings.weight.copy_(torch.from_numpy(U))
+        mf.item_embeddings.weight.copy_(torch.from_numpy(I))
+    return mf.to(device)
+
+
+def ranking_dataset(g, n_users, n_items):
+    train_ds = datasets.UserItemInteractionsDataset(torch.from_numpy(g["train"]),
+                                                    number_of_users=n_users, number_of_items=n_items)
+    test_ds = datasets.UserItemInteractionsDataset(torch.from_numpy(g["test"]),
+                                                   number_of_users=n_users, number_of_items=n_items)
+    return datasets.RankingDataset(test_ds, frozen=train_ds)
+
+
+def assert_topk_gap_exact(got, ref, U, I, frozen_csr, tol):
+    """got == ref except where the reference's own ordering is within tol."""
+    S = U.astype(np.float64) @ I.astype(np.float64).T
+    rowptr, cols = frozen_csr
+    bad = 0
+    for u in range(ref.shape[0]):
+        if np.array_equal(got[u], ref[u]):
+            continue
+        s = S[u].copy()
+        s[cols[rowptr[u]:rowptr[u + 1]]] = -np.inf
+        # the returned list must be a valid top-k under a tol-perturbation:
+        # sorted by score within tol, and no omitted item clearly better
+        gs = s[got[u]]
+        assert np.all(np.diff(gs) <= 2 * tol), u
+        kth = np.sort(s)[::-1][len(ref[u]) - 1]
+        assert np.all(gs >= kth - 2 * tol), u
+        must = np.nonzero(s > kth + 2 * tol)[0]
+        assert set(must.tolist()) <= set(got[u].tolist()), u
+        bad += 1
+    return bad
+
+
+@pytest.mark.parametrize("d", [32, 64, 128])
+def test_mf_forward_golden(d):
+    g = load(f"mf_forward_d{d}")
+    mf = mf_from(g["U"], g["I"])
+    with torch.no_grad():
+        out = mf(torch.from_numpy(g["uid"]), torch.from_numpy(g["iid"])).cpu().numpy()
+    scale = np.abs(g["U"][g["uid"]] * g["I"][g["iid"]]).sum(axis=1)
+    assert np.all(np.abs(out - g["out"]) <= 5e-7 * scale)
+
+
+def test_mf_backward_matches_torch():
+    g = load("mf_forward_d64")
+    mf = mf_from(g["U"], g["I"])
+    uid, iid = torch.from_numpy(g["uid"]), torch.from_numpy(g["iid"])
+    w = torch.linspace(-1, 1, uid.numel())
+    (mf(uid, iid) * w.to(DEV)).sum().backward()
+    U = torch.from_numpy(g["U"]).requires_grad_()
+    I = torch.from_numpy(g["I"]).requires_grad_()
+    ((U[uid] * I[iid]).sum(1) * w).sum().backward()
+    assert torch.allclose(mf.user_embeddings.weight.grad.cpu(), U.grad, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(mf.item_embeddings.weight.grad.cpu(), I.grad, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["recs_int_k10", "recs_int_k100"])
+def test_recommendations_integer_exact(name):
+    g = load(name)
+    U, I, k = g["U"], g["I"], int(g["k"])
+    rds = ranking_dataset(g, U.shape[0], I.shape[0])
+    recs = train.get_model_recommendations(rds, mf_from(U, I), k)
+    assert recs.dtype == torch.int64 and recs.device.type == "cpu"
+    assert np.array_equal(recs.numpy(), g["recs"])
+
+
+@pytest.mark.parametrize("name", ["recs_float_k10", "recs_float_k100"])
+def test_recommendations_float_gap_exact(name):
+    g = load(name)
+    U, I, k = g["U"], g["I"], int(g["k"])
+    rds = ranking_dataset(g, U.shape[0], I.shape[0])
+    recs = train.get_model_recommendations(rds, mf_from(U, I), k).numpy()
+    rowptr, cols = rds.exclusion_csr()
+    tol = 1e-5 * max(1.0, float(np.abs(U).max() * np.abs(I).max() * U.shape[1] / 8))
+    bad = assert_topk_gap_exact(recs, g["recs"], U, I, (rowptr.numpy(), cols.numpy()), tol)
+    assert bad <= U.shape[0] // 16
+
+
+def test_ml100k_config1_end_to_end():
+    """configs[0]: ML-100K-shaped MF d=32, top-10, cosine ILD + accuracy and
+    diversity metrics, all through the drop-in API."""
+    g = load("ml100k_cfg1")
+    U, I = g["U"], g["I"]
+    nu, ni = U.shape[0], I.shape[0]
+    rds = ranking_dataset(g, nu, ni)
+    mf = mf_from(U, I)
+    recs = train.get_model_recommendations(rds, mf, 10)
+    rowptr, cols = rds.exclusion_csr()
+    bad = assert_topk_gap_exact(recs.numpy(), g["recs"], U, I, (rowptr.numpy(), cols.numpy()), 2e-5)
+    assert bad <= nu // 50
+    # ILD with the reference's dense cosine D (torch fp32, built like the reference)
+    It = torch.from_numpy(I)
+    En = It / It.norm(dim=1, keepdim=True)
+    Dc = 1.0 - En @ En.T
+    ild = losses.IntraListDiversityScore(distance_matrix=Dc, reduction="none")
+    ref_recs = torch.from_numpy(g["recs"])
+    assert np.array_equal(ild(None, ref_recs).cpu().numpy(), g["ild"])
+    (res,) = train.recommendations_score_loop(rds, mf, [ild], 10)
+    same = (recs.numpy() == g["recs"]).all(axis=1)
+    assert np.array_equal(res.cpu().numpy()[same], g["ild"][same])
+    # ILD with D computed on the fly from the embeddings (bf16 Gram tiles)
+    lazy = losses.IntraListDiversityScore(distance_matrix=EmbeddingDistance(It, "cosine"),
+                                          reduction="none")
+    assert np.allclose(lazy(None, ref_recs).cpu().numpy(), g["ild"], rtol=1e-5, atol=2e-6)
+    # accuracy metrics on the reference's lists
+    te = torch.from_numpy(g["test"])
+    for fn, key in ((metrics.precision_at_k, "precision"), (metrics.recall_at_k, "recall"),
+                    (metrics.average_precision_at_k, "ap"),
+                    (metrics.normalized_discounted_cumulative_gain, "ndcg")):
+        assert np.allclose(fn(te, ref_recs).cpu().numpy(), g[key], rtol=1e-6, atol=1e-7), key
+    full = datasets.UserItemInteractionsDataset(torch.cat([torch.from_numpy(g["train"]), te]),
+                                                number_of_users=nu, number_of_items=ni)
+    assert float(metrics.EntropyDiversityScore(dataset=full)(te, ref_recs)) == pytest.approx(
+        float(g["entropy"]), rel=1e-6)
+    assert float(metrics.PRI(dataset=full)(te, ref_recs)) == pytest.approx(float(g["pri"]), rel=1e-5)
+    assert float(metrics.MeanAveragePrecisionAtKScore()(te, ref_recs)) == pytest.approx(
+        float(g["map"]), rel=1e-6)
+
+
+@pytest.mark.parametrize("k", [1, 2, 10, 100])
+def test_ild_dense_golden_bit_exact(k):
+    g = load(f"ild_dense_k{k}")
+    D = torch.from_numpy(g["D"])
+    recs = torch.from_numpy(g["recs"]).to(DEV)
+    got = losses.IntraListDiversityScore(distance_matrix=D, reduction="none")(None, recs)
+    assert np.array_equal(got.cpu().numpy(), g["out"], equal_nan=True)
+    if k > 1:
+        s = losses.IntraListDiversityScore(distance_matrix=D, reduction="sum")(None, recs)
+        assert float(s) == pytest.approx(float(g["sum"]), rel=1e-6)
+
+
+def test_ild_labels_golden():
+    g = load("ild_labels")
+    recs = torch.from_numpy(g["recs"])
+    lab = torch.from_numpy(g["labels"])
+    got = losses.IntraListDiversityScore(distance_matrix=LabelEquality(lab), reduction="none")
+    assert np.array_equal(got(None, recs).cpu().numpy(), g["out"])
+    ds = datasets.UserItemInteractionsDataset(
+        torch.LongTensor([[0, 0]]), number_of_items=lab.numel(),
+        item_features=datasets.Features(lab[:, None].float(), ["partition"]))
+    unf = losses.IntraListBinaryUnfairnessScore(dataset=ds, reduction="none")
+    assert np.array_equal(unf(None, recs).cpu().numpy(), g["out"])
+
+
+def test_ild_cosine_golden():
+    g = load("ild_cosine")
+    recs = torch.from_numpy(g["recs"])
+    dense = losses.IntraListDiversityScore(distance_matrix=torch.from_numpy(g["D"]), reduction="none")
+    assert np.array_equal(dense(None, recs).cpu().numpy(), g["out"])
+    lazy = losses.IntraListDiversityScore(
+        distance_matrix=EmbeddingDistance(torch.from_numpy(g["E"]), "cosine"), reduction="none")
+    assert np.allclose(lazy(None, recs).cpu().numpy(), g["out"], rtol=1e-5, atol=2e-6)
+
+
+def test_bpr_step_golden():
+    g = load("bpr_step")
+    mf = mf_from(g["U0"], g["I0"])
+    opt = torch.optim.Adam(mf.parameters(), lr=1e-3)
+    U, I = mf.user_embeddings.weight, mf.item_embeddings.weight
+    U.grad, I.grad = torch.zeros_like(U), torch.zeros_like(I)
+    B = g["uid"].size
+    lv, hit = ops.bpr_fwd_bwd(U.data, I.data, *(torch.from_numpy(g[n]).to(DEV)
+                                                 for n in ("uid", "pid", "nid")), 1.0 / B, U.grad, I.grad)
+    assert float(lv.sum() / B) == pytest.approx(float(g["loss"]), rel=1e-6)
+    assert float(hit.float().mean()) == pytest.approx(float(g["auc"]), abs=1e-7)
+    assert np.allclose(U.grad.cpu().numpy(), g["gU"], rtol=1e-5, atol=1e-8)
+    assert np.allclose(I.grad.cpu().numpy(), g["gI"], rtol=1e-5, atol=1e-8)
+    train.fused_adam_step(opt)
+    assert np.allclose(U.detach().cpu().numpy(), g["U1"], rtol=0, atol=1e-6)
+    assert np.allclose(I.detach().cpu().numpy(), g["I1"], rtol=0, atol=1e-6)
+
+
+def test_pair_wise_train_loop_golden():
+    g = load("bpr_loop")
+    tr = torch.from_numpy(g["train"])
+    data = datasets.UserItemInteractionsDataset(
+        tr, user_features=datasets.Features(torch.zeros(12, 1), ["x"]),
+        item_features=datasets.Features(torch.zeros(40, 1), ["x"]))
+    mf = mf_from(g["U0"], g["I0"])
+    random.seed(int(g["seed"]))
+    pw = datasets.PairWiseDataset(data, max_sampled=int(g["max_sampled"]))
+    opt = torch.optim.Adam(mf.parameters(), lr=float(g["lr"]))
+    mean_loss, (mean_auc,) = train.pair_wise_train_loop(
+        pw, mf, losses.LogSigmoidDifferenceLoss(), opt, scores=[metrics.AUCScore()],
+        batch_size=int(g["batch_size"]))
+    assert mean_loss == pytest.approx(float(g["mean_loss"]), rel=1e-5)
+    assert mean_auc == pytest.approx(float(g["mean_auc"]), abs=1e-6)
+    assert np.allclose(mf.user_embeddings.weight.detach().cpu().numpy(), g["U1"], atol=1e-5)
+    assert np.allclose(mf.item_embeddings.weight.detach().cpu().numpy(), g["I1"], atol=1e-5)
+
+
+def test_rank_metrics_against_oracle_formulas():
+    rng = np.random.default_rng(3)
+    nu, ni, k = 200, 500, 37
+    recs = torch.from_numpy(np.stack([rng.choice(ni, k, replace=False) for _ in range(nu)]))
+    inter = torch.from_numpy(np.stack([np.repeat(np.arange(nu), 12),
+                                       rng.integers(0, ni, nu * 12)], 1))
+    inter[inter[:, 0] == 5, 0] = 6  # user 5 has no positives: recall NaN
+    p, r, ap, nd = (f(inter, recs).cpu().numpy() for f in (
+        metrics.precision_at_k, metrics.recall_at_k, metrics.average_precision_at_k,
+        metrics.normalized_discounted_cumulative_gain))
+    for u in range(nu):
+        pos = inter[inter[:, 0] == u, 1].numpy()
+        rel = np.isin(recs[u].numpy(), pos).astype(np.float64)
+        assert p[u] == pytest.approx(rel.sum() / k, rel=1e-6)
+        if len(pos):
+            assert r[u] == pytest.approx(rel.sum() / len(pos), rel=1e-6)
+        else:
+            assert np.isnan(r[u])
+        cum = np.cumsum(rel) / np.arange(1, k + 1)
+        assert ap[u] == pytest.approx(cum.sum() / k, rel=1e-5, abs=1e-7)
+        disc = 1 / np.log2(np.arange(2, k + 2))
+        assert nd[u] == pytest.approx((rel * disc).sum() / disc.sum(), rel=1e-5, abs=1e-7)
+
+
+def test_score_topk_api_exclusion_and_user_subset():
+    rng = np.random.default_rng(11)
+    U = rng.integers(-3, 4, size=(50, 64)).astype(np.float32)
+    I = rng.integers(-3, 4, size=(3000, 64)).astype(np.float32)
+    mf = mf_from(U, I)
+    frozen = [sorted(set(rng.integers(0, 3000, 40).tolist())) for _ in range(20)]
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    uids = torch.arange(10, 30)
+    items, scores = mf.score_topk(25, user_ids=uids, exclude=(torch.from_numpy(rowptr),
+                                                             torch.from_numpy(cols)))
+    ref = oracle.recommend_topk(U[10:30], I, 25, frozen=frozen)
+    assert np.array_equal(items.cpu().numpy(), ref)

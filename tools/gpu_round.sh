@@ -1,0 +1,11 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprofv3 kernel summary.
+# Every GPU step has its own time limit; the first failure ends the script.
+set -e
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1
+cd /tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1
