@@ -42,7 +42,10 @@ def _headers_mtime() -> float:
 
 def _compile(src: Path, verbose: bool, obj_dir: Path = OBJ_DIR, extra=()) -> Path:
     obj = obj_dir / (src.stem + ".o")
-    if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
+    stamp = obj_dir / "flags.txt"
+    same_flags = stamp.exists() and stamp.read_text() == " ".join(extra)
+    if same_flags and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime,
+                                                                  _headers_mtime()):
         return obj
     cmd = [HIPCC, *CFLAGS, *extra, "-c", str(src), "-o", str(obj)]
     if verbose:
@@ -53,18 +56,25 @@ def _compile(src: Path, verbose: bool, obj_dir: Path = OBJ_DIR, extra=()) -> Pat
     return obj
 
 
-def build(jobs: int = 4, verbose: bool = False, diag: bool = False) -> Path:
-    """Build the product library, or with diag=True the instrumented
-    libdivrec_hip_diag.so (-DDR_TOPK_DIAG; profiling only, never loaded by
-    the product path unless DIVREC_HIP_LIB points at it)."""
-    obj_dir = OBJ_DIR.parent / "obj_diag" if diag else OBJ_DIR
-    lib_path = LIB_DIR / "libdivrec_hip_diag.so" if diag else LIB_PATH
-    extra = ("-DDR_TOPK_DIAG",) if diag else ()
+def build(jobs: int = 4, verbose: bool = False, diag: bool = False, variant: str = "",
+          defines=()) -> Path:
+    """Build the product library; with diag=True the instrumented
+    libdivrec_hip_diag.so (-DDR_TOPK_DIAG); with variant=NAME and defines
+    (KEY=VAL strings) libdivrec_hip_NAME.so for tools/variant_bench.py. Diag
+    and variant libraries are measurement tools: the product path loads them
+    only when DIVREC_HIP_LIB points at one."""
+    defines = tuple(defines)
+    if diag:
+        variant, defines = variant or "diag", ("DR_TOPK_DIAG",) + defines
+    obj_dir = OBJ_DIR.parent / f"obj_{variant}" if variant else OBJ_DIR
+    lib_path = LIB_DIR / f"libdivrec_hip_{variant}.so" if variant else LIB_PATH
+    extra = tuple(f"-D{d}" for d in defines)
     obj_dir.mkdir(parents=True, exist_ok=True)
     LIB_DIR.mkdir(parents=True, exist_ok=True)
     srcs = sorted(CSRC.glob("*.hip"))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda s: _compile(s, verbose, obj_dir, extra), srcs))
+    (obj_dir / "flags.txt").write_text(" ".join(extra))
     newest = max(o.stat().st_mtime for o in objs)
     if lib_path.exists() and lib_path.stat().st_mtime >= newest:
         return lib_path
@@ -84,8 +94,11 @@ def main() -> int:
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--diag", action="store_true", help="build the instrumented diag library")
+    ap.add_argument("--variant", default="", help="build libdivrec_hip_<NAME>.so")
+    ap.add_argument("-D", dest="defines", action="append", default=[],
+                    help="KEY=VAL preprocessor define for a variant build (repeatable)")
     args = ap.parse_args()
-    path = build(args.jobs, args.verbose, args.diag)
+    path = build(args.jobs, args.verbose, args.diag, args.variant, args.defines)
     print(path)
     return 0
 

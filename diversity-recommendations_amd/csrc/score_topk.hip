@@ -4,28 +4,37 @@
 // with MatrixFactorization.forward (matrix_factorization.py:26-28) and keeps
 // candidates[argsort(scores, descending=True)][:k].
 //
-// Two kernels:
+// Kernels:
 //
 // score_scan_kernel — one 512-thread workgroup (8 waves, two per SIMD) owns
-//   UPWG = 8*NU_T*32 users and streams one chunk of the item catalog.
+//   UPWG = 8*NU_T*32 users (1024 for d <= 128) and streams one chunk of the
+//   item catalog, so every item byte staged in LDS feeds UPWG flop.
 //   * Each wave keeps the bf16 embeddings of its NU_T*32 users resident in
 //     registers as MFMA B fragments for the whole scan.
 //   * Item rows go HBM -> LDS by LDS-DMA (global_load_lds_dwordx4) into a ring
-//     of 16-KB stages filled kRing-1 stages ahead; the LDS image is
+//     of 32-KB stages filled kRing-1 = 3 stages ahead; the LDS image is
 //     XOR-swizzled through the per-lane source address so the A-fragment
 //     ds_read_b128s are bank-conflict-free. All 8 waves share every stage.
+//     A fragments are read two k-steps ahead of the MFMAs that use them.
 //   * v_mfma_f32_32x32x16_bf16 puts items on M and users on N, so a lane holds
 //     16 scores of ONE user: the hot epilogue is a 16-way max and one compare
 //     with that user's running threshold. Scores never leave registers. The
 //     two waves of a SIMD cover each other's epilogues.
-//   * Survivors (rare once thresholds settle) go to a per-wave LDS queue; the
-//     queue is drained in batches into per-user candidate buffers in HBM. When
-//     a buffer nears capacity the wave compacts it with an in-register radix
-//     select, keeping only keys that can still reach the top k, and raises the
-//     user's threshold to the selected bound.
+//   * Survivors are stored straight into per-user candidate buffers in HBM
+//     (slot from a per-user LDS counter). Once a buffer holds more than
+//     k + kSlack + kFlushGap keys the wave compacts it with an in-register
+//     radix select, keeping only keys that can still reach the top k, and
+//     raises the user's threshold to the selected bound.
+//   * Seeded thresholds (SEEDED = true): for large catalogs dr_score_topk
+//     first scans a sample (the slice's first S items) and
+//     topk_threshold_kernel sets each user's starting threshold just below its
+//     k-th best sample score. Every item of the true top k scores at least
+//     that much (the sample is part of the catalog), so the main scan skips
+//     the dense early survivor stream of a scan that starts at -inf.
 //   * All VMEM traffic inside the scan (LDS-DMA and candidate stores) is
 //     issued from inline asm and counted by the wave, so each stage wait is an
 //     exact s_waitcnt vmcnt(N): no drain of the ring.
+// topk_threshold_kernel — one wave per user: k-th best key of the sample scan.
 // topk_finalize_kernel — one wave per user: gather the candidates of all
 //   chunks, drop excluded items, bitonic sort, write the k best.
 //
@@ -56,14 +65,44 @@ enum {
   kDgNTiles, kDgNEnqueue, kDgNDrain, kDgNFlush, kDgNStages, kDgSlots = 16
 };
 
+// Geometry knobs. The defaults are the product configuration; the -D
+// overrides exist so tools/variant_bench.py can time alternatives side by side
+// (build_native.py --variant NAME -D KEY=VAL).
+#ifndef DR_STAGE_BYTES
+#define DR_STAGE_BYTES 32768  // one LDS ring slot
+#endif
+#ifndef DR_RING
+#define DR_RING 4  // ring slots (kRing - 1 stages in flight)
+#endif
+#ifndef DR_NUT
+#define DR_NUT 4  // user tiles of 32 per wave for d <= 128
+#endif
+#ifndef DR_PRIO
+#define DR_PRIO 0  // static s_setprio 1 for waves 4-7 (measured: no gain)
+#endif
+#ifndef DR_APIPE
+#define DR_APIPE 1  // A fragments read two k-steps ahead
+#endif
+#ifndef DR_FLUSH_GAP
+#define DR_FLUSH_GAP 96  // new keys a buffer takes past k + kSlack before compaction
+#endif
+#ifndef DR_PREPASS
+#define DR_PREPASS 0  // seed thresholds from a sample scan (measured: 1-4% slower)
+#endif
+#ifndef DR_COMPACT_INLINE
+#define DR_COMPACT_INLINE __noinline__
+#endif
+
 constexpr int kWaves = 8;  // two waves per SIMD: 256-register budget each
 constexpr int kThreads = kWaves * 64;
 constexpr int kTileItems = 32;
-constexpr int kStageBytes = 16384;                  // one LDS ring slot
-constexpr int kLpt = kStageBytes / 16 / kThreads;  // LDS-DMA per thread per stage (= 2)
-constexpr int kRing = 4;                            // stages resident / in flight
-constexpr int kQcap = 512;                          // per-wave survivor queue (entries)
-constexpr int kSlack = 32;                          // keys kept beyond k by a compaction
+constexpr int kStageBytes = DR_STAGE_BYTES;
+constexpr int kLpt = kStageBytes / 16 / kThreads;  // LDS-DMA per thread per stage
+constexpr int kRing = DR_RING;
+constexpr int kSlack = 32;   // keys kept beyond k by a compaction
+constexpr int kFlushGap = DR_FLUSH_GAP;
+static_assert(kLpt >= 1 && kStageBytes % (16 * kThreads) == 0, "stage geometry");
+static_assert(kRing >= 2, "ring depth");
 
 template <int D>
 struct TileGeom {
@@ -74,15 +113,15 @@ struct TileGeom {
   static constexpr int RPB = (2 * D >= 256) ? 1 : 256 / (2 * D);  // rows per 256-B bank row
   static constexpr int SWM = (CPR < 16 ? CPR : 16) - 1;
   static constexpr int MARGIN = SR * kTileItems;  // max new keys per user per stage
+  static_assert(SR >= 1, "a stage holds at least one tile");
   // physical chunk = logical chunk ^ swz(row): spreads the 32 rows that one
   // A-fragment ds_read_b128 touches over distinct 16-B bank slots.
   __device__ static int swz(int r) { return (r / RPB) & SWM; }
 };
 
-template <int D>
-struct NuT {  // user tiles (of 32) per wave: B fragments NU_T*KSTEPS*4 <= 64 VGPRs
-  static constexpr int value = (D >= 256) ? 1 : 2;
-};
+// User tiles (of 32) per wave. The B fragments take NU_T*KSTEPS*4 VGPRs (128 at
+// d=128, NU_T=4) and the accumulators NU_T*16.
+constexpr int nut_for(int d) { return d >= 256 ? 2 : DR_NUT; }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -92,28 +131,23 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // prove a C++ ds_read does not alias an in-flight LDS-DMA); the wave counts
 // every instruction it issues and waits with exact counts. M0 is used by no
 // other code in the kernel.
-__device__ __forceinline__ void glds16(const void* src, uint32_t lds_wave_base) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_wave_base);
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-               :
-               : "v"(src), "s"(m0)
-               : "memory", "m0");
-#pragma clang diagnostic pop
-}
 __device__ __forceinline__ void st64(uint64_t* p, uint64_t v) {
   asm volatile("global_store_dwordx2 %0, %1, off" : : "v"(p), "v"(v) : "memory");
-}
-// A store of more than 64 data bits reads its data VGPRs after issue: the
-// trailing s_nop 1 keeps hipcc's next instruction from overwriting them first.
-__device__ __forceinline__ void st128(void* p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
 }
 __device__ __forceinline__ u32x4 ds_read_b128_asm(uint32_t lds_addr) {
   u32x4 v;
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr));
   return v;
+}
+// LDS waits that name the fragment they retire ("+v"): no consumer of it can
+// be scheduled above the wait. lgkmcnt(1) = every LDS read but the youngest
+// has returned (LDS reads return in order; extra younger reads only make the
+// wait stricter).
+__device__ __forceinline__ void lds_wait1(u32x4& v) {
+  asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(v) : : "memory");
+}
+__device__ __forceinline__ void lds_wait0(u32x4& v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v) : : "memory");
 }
 
 // s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at their maxima).
@@ -122,40 +156,57 @@ __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
-template <int N>
-__device__ __forceinline__ void wait_vmcnt_le(int n) {  // n is wave-uniform
-  if constexpr (N == 0) {
-    wait_vmcnt<0>();
-  } else {
-    if (n >= N) wait_vmcnt<N>();
-    else wait_vmcnt_le<N - 1>(n);
-  }
+// Wait until at most n (wave-uniform) VMEM ops are outstanding, rounding n
+// down to a power of two (waits for a little more than required, always
+// correct): six scalar compares instead of a 64-step ladder at every stage.
+__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
+  if (n >= 32) wait_vmcnt<32>();
+  else if (n >= 16) wait_vmcnt<16>();
+  else if (n >= 8) wait_vmcnt<8>();
+  else if (n >= 4) wait_vmcnt<4>();
+  else if (n >= 2) wait_vmcnt<2>();
+  else if (n >= 1) wait_vmcnt<1>();
+  else wait_vmcnt<0>();
 }
-// Wait until at most n (wave-uniform) VMEM ops are outstanding; n >= 63
-// saturates at 63, which waits for more than required (still correct).
-__device__ __forceinline__ void wait_vmcnt_dyn(int n) { wait_vmcnt_le<63>(n); }
 
 // Issue the LDS-DMA of one stage: rows [row0, row0 + SR*32) of the slice into
 // the ring slot at LDS byte address `lds_stage`. The image is lane-linear
 // (glds writes base + lane*16); the swizzle is on the SOURCE address
 // (cdna_hip_programming.md §5.4 rule 21). Rows past the slice end are
 // clamped to its last row; their scores are masked in the epilogue.
+// Addressing is SGPR base (the stage's first row) + a 32-bit per-lane offset
+// recomputed at every stage from the thread id: the empty asm makes the id
+// opaque, so hipcc cannot hoist 64-bit per-lane addresses out of the tile loop
+// (they cost registers the loop does not have, and their spill reloads wait
+// vmcnt(0), draining the ring).
 template <int D>
 __device__ __forceinline__ void issue_stage(const __bf16* __restrict__ I, int64_t n_items,
                                             int64_t row0, uint32_t lds_stage) {
   using G = TileGeom<D>;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
+  constexpr int ROWS = G::SR * kTileItems;
+  uint32_t tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = (int)(tid & 63u);
+  const int wave = (int)(__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
+  const char* base = reinterpret_cast<const char*>(I + row0 * D);
+  const int64_t left = n_items - 1 - row0;
+  const int rmax = left < ROWS - 1 ? (int)left : ROWS - 1;
 #pragma unroll
   for (int j = 0; j < kLpt; ++j) {
     const int wave_first = j * kThreads + wave * 64;  // wave-uniform chunk index
-    const int idx = wave_first + (tid & 63);
+    const int idx = wave_first + lane;
     const int r = idx / G::CPR;
-    const int pc = idx % G::CPR;
-    const int lc = pc ^ G::swz(r & 31);
-    int64_t row = row0 + r;
-    row = row < n_items ? row : n_items - 1;
-    glds16(I + row * D + lc * 8, lds_stage + wave_first * 16);
+    const int lc = (idx % G::CPR) ^ G::swz(r & 31);
+    const int rr = r < rmax ? r : rmax;
+    const uint32_t off = (uint32_t)(rr * (2 * D) + lc * 16);
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_stage + wave_first * 16);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :
+                 : "v"(off), "s"(base), "s"(m0)
+                 : "memory", "m0");
+#pragma clang diagnostic pop
   }
 }
 
@@ -193,7 +244,7 @@ struct CompactResult {
 // score is the new threshold: >= k kept keys rank above any later item of
 // equal or lower score. Excluded items are dropped first.
 template <int P>
-__device__ __noinline__ CompactResult compact_buffer(uint64_t* __restrict__ buf, int n_in, int k,
+__device__ DR_COMPACT_INLINE CompactResult compact_buffer(uint64_t* __restrict__ buf, int n_in, int k,
                                                      const int32_t* __restrict__ ex, int exn,
                                                      uint32_t* __restrict__ hist) {
   const int lane = dr::lane_id();
@@ -282,29 +333,6 @@ __device__ __noinline__ CompactResult compact_buffer(uint64_t* __restrict__ buf,
   return res;
 }
 
-// Drain a wave's survivor queue into the per-user candidate buffers (cold
-// path). Returns the number of store instructions issued (one per 64 entries).
-__device__ __noinline__ int drain_queue(const uint64_t* __restrict__ qkey,
-                                        const uint32_t* __restrict__ qslot,
-                                        uint32_t* __restrict__ ucnt, int qlen,
-                                        uint64_t* __restrict__ cbase, int cap) {
-  const int lane = dr::lane_id();
-  wave_lds_sync();
-  int n = 0;
-  for (int b0 = 0; b0 < qlen; b0 += 64) {
-    const int i = b0 + lane;
-    if (i < qlen) {
-      const uint64_t key = qkey[i];
-      const uint32_t slot = qslot[i];
-      const uint32_t pos = atomicAdd(&ucnt[slot], 1u);
-      st64(cbase + (size_t)slot * cap + pos, key);
-    }
-    ++n;
-  }
-  wave_lds_sync();
-  return n;
-}
-
 struct TopkArgs {
   const __bf16* U;
   const int64_t* user_ids;
@@ -319,41 +347,54 @@ struct TopkArgs {
   int n_chunks;
   int64_t chunk_items;  // multiple of the stage's item count
   int64_t n_ublocks;
+  const float* init_thr;  // [n_users_pad] starting thresholds (SEEDED scans only)
   uint64_t* cand;  // [n_chunks][n_users_pad][CAP] keys (unsorted)
   int32_t* cnt;    // [n_chunks][n_users_pad] valid keys per buffer
   uint64_t* diag;  // [gridDim.x * kWaves][kDgSlots] in DR_TOPK_DIAG builds
 };
 
-template <int D, int CAP>
+template <int D, int CAP, bool SEEDED>
 __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
   using G = TileGeom<D>;
-  constexpr int NU_T = NuT<D>::value;
+  constexpr int NU_T = nut_for(D);
   constexpr int KS = G::KSTEPS;
   constexpr int SR = G::SR;
   constexpr int UPW = NU_T * 32;      // users per wave
   constexpr int UPWG = UPW * kWaves;  // users per workgroup
-  constexpr int FLUSH_AT = CAP - G::MARGIN;        // compact when a buffer holds more
-  constexpr int WARM = FLUSH_AT / kTileItems;      // warm-up tiles written without a test
-  constexpr int P = CAP / 64;                      // keys per lane in a compaction
+  constexpr int P = CAP / 64;         // keys per lane in a compaction
   constexpr int RING_BYTES = kRing * kStageBytes;
-  constexpr int WAVE_BYTES = kQcap * 8 + kQcap * 4 + UPW * 4 + 256 * 4;
+  constexpr int WAVE_BYTES = UPW * 4 + 256 * 4;  // per-user key counts + radix histogram
   static_assert(RING_BYTES + kWaves * WAVE_BYTES <= 163840, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[RING_BYTES + kWaves * WAVE_BYTES];
+
+  // A buffer is compacted once it holds more than flush_at keys; a stage adds
+  // at most MARGIN keys per user, so flush_at + MARGIN <= CAP. A small gap
+  // above k + kSlack keeps the thresholds close to the running k-th score.
+  // Unseeded scans start at -inf: every score of the first stages is a
+  // survivor until the first compaction sets a real threshold.
+  int flush_at = a.k + kSlack + kFlushGap;
+  flush_at = flush_at < CAP - G::MARGIN ? flush_at : CAP - G::MARGIN;
 
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5;
   const int col = lane & 31;
+#if DR_PRIO
+  // The second-dispatched half of the workgroup loses VALU arbitration to its
+  // SIMD partner on every segment; one static priority bump evens the pair
+  // (cdna_hip_programming.md T5, static form). Wave-uniform by readfirstlane.
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
   char* wbase = smem + RING_BYTES + wave * WAVE_BYTES;
-  uint64_t* qkey = reinterpret_cast<uint64_t*>(wbase);
-  uint32_t* qslot = reinterpret_cast<uint32_t*>(wbase + kQcap * 8);
-  uint32_t* ucnt = reinterpret_cast<uint32_t*>(wbase + kQcap * 12);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(wbase + kQcap * 12 + UPW * 4);
+  uint32_t* ucnt = reinterpret_cast<uint32_t*>(wbase);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(wbase + UPW * 4);
   const uint32_t lds_ring = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
-  uint32_t a_off[KS];  // this lane's A-fragment byte offset for k-step s in a tile
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-    a_off[s] = (uint32_t)(col * (2 * D) + (((2 * s + h) ^ G::swz(col)) << 4));
+  // This lane's A-fragment byte offset for k-step s in a tile is
+  // col*2D + ((2s + h) ^ swz(col)) * 16 = a_row + ((2s) ^ a_sw) * 16: two VALU
+  // per read instead of KS resident offsets (registers are the budget here).
+  const uint32_t a_row = (uint32_t)(col * (2 * D));
+  const uint32_t a_sw = (uint32_t)(h ^ G::swz(col));
+  auto a_off = [&](int s) -> uint32_t { return a_row + ((((uint32_t)(2 * s)) ^ a_sw) << 4); };
 
 #ifdef DR_TOPK_DIAG
   uint64_t dg[kDgSlots] = {};
@@ -374,6 +415,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
 
     // Resident B fragments: lane holds user (ut*32+col), k = 16s + 8h .. +7.
     bf16x8 bfr[NU_T][KS];
+    float thr[NU_T];
 #pragma unroll
     for (int ut = 0; ut < NU_T; ++ut) {
       const int64_t pos = upos0 + ut * 32 + col;
@@ -382,15 +424,12 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       const uint4* src = reinterpret_cast<const uint4*>(a.U + row * D + 8 * h);
 #pragma unroll
       for (int s = 0; s < KS; ++s) bfr[ut][s] = __builtin_bit_cast(bf16x8, src[2 * s]);
+      thr[ut] = SEEDED ? a.init_thr[pos] : -INFINITY;
     }
     // Retire those loads where the compiler can see it (else it waits for them
     // inside the loop, draining the ring).
     wait_vmcnt<0>();
     for (int s = lane; s < UPW; s += 64) ucnt[s] = 0;
-    float thr[NU_T];
-#pragma unroll
-    for (int ut = 0; ut < NU_T; ++ut) thr[ut] = -INFINITY;
-    int qlen = 0;       // survivor queue length (wave-uniform)
     int vmc = 0;        // VMEM instructions issued by this wave in this unit
     int vm_done = 0;    // every op issued before this count has completed
     int vs[kRing - 1];  // vmc right after each outstanding stage's DMA
@@ -403,12 +442,29 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       const uint32_t tb = lds_ring + ((t / SR) % kRing) * kStageBytes + (t % SR) * G::TILE_BYTES;
 #pragma unroll
       for (int ut = 0; ut < NU_T; ++ut) acc[ut] = f32x16{};
+#if DR_APIPE
+      // Fragment s is read two k-steps before its MFMAs; each wait retires
+      // exactly the fragment the next MFMAs consume.
+      u32x4 af[KS];
+      af[0] = ds_read_b128_asm(tb + a_off(0));
+      if constexpr (KS > 1) af[1] = ds_read_b128_asm(tb + a_off(1));
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        if (s + 1 < KS) lds_wait1(af[s]);
+        else lds_wait0(af[s]);
+        if (s + 2 < KS) af[s + 2] = ds_read_b128_asm(tb + a_off(s + 2));
+#pragma unroll
+        for (int ut = 0; ut < NU_T; ++ut)
+          acc[ut] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[s]),
+                                                            bfr[ut][s], acc[ut], 0, 0, 0);
+      }
+#else
       constexpr int HALF = KS >= 4 ? KS / 2 : KS;
 #pragma unroll
       for (int s0 = 0; s0 < KS; s0 += HALF) {
         u32x4 af[HALF];
 #pragma unroll
-        for (int s = 0; s < HALF; ++s) af[s] = ds_read_b128_asm(tb + a_off[s0 + s]);
+        for (int s = 0; s < HALF; ++s) af[s] = ds_read_b128_asm(tb + a_off(s0 + s));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -418,6 +474,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
             acc[ut] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
                 __builtin_bit_cast(bf16x8, af[s]), bfr[ut][s0 + s], acc[ut], 0, 0, 0);
       }
+#endif
     };
 
     // -------------------------------------------------------------- cold paths
@@ -438,24 +495,16 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       wave_lds_sync();
 #pragma unroll
       for (int u2 = 0; u2 < NU_T; ++u2)
-        if (u2 == ut && col == c) thr[u2] = r.thr;
+        if (u2 == ut && col == c) thr[u2] = fmaxf(thr[u2], r.thr);  // both bounds are valid
       DG_ADD(kDgFlush, t_f);
       DG_CNT(kDgNFlush);
-    };
-
-    auto drain = [&]() {
-      DG_T0(t_d);
-      vmc += drain_queue(qkey, qslot, ucnt, qlen, cbase, CAP);
-      qlen = 0;
-      DG_ADD(kDgDrain, t_d);
-      DG_CNT(kDgNDrain);
     };
 
     auto check_compact = [&]() {
 #pragma unroll
       for (int ut = 0; ut < NU_T; ++ut) {
         const uint32_t c_cnt = ucnt[ut * 32 + col];
-        uint64_t need = __ballot(c_cnt > (uint32_t)FLUSH_AT) & 0xffffffffull;
+        uint64_t need = __ballot(c_cnt > (uint32_t)flush_at) & 0xffffffffull;
         while (need) {
           const int c = __builtin_ctzll(need);
           need &= need - 1;
@@ -465,41 +514,6 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
     };
 
     // -------------------------------------------------------------- epilogues
-    // Warm-up: the first WARM tiles are written to the buffers unconditionally
-    // (position = item offset), then every buffer is compacted once.
-    auto warm_fill = [&](int t, f32x16 (&acc)[NU_T]) {
-      const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
-      const int valid = (int)((i_end - tile0) < kTileItems ? (i_end - tile0) : kTileItems);
-      const uint32_t gbase = (uint32_t)(a.item_base + tile0);
-#pragma unroll
-      for (int ut = 0; ut < NU_T; ++ut) {
-        uint64_t* dst = cbase + (size_t)(ut * 32 + col) * CAP + t * kTileItems;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          uint64_t kk[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int row = 8 * g + 4 * h + j;
-            kk[j] = row < valid ? dr::make_key(acc[ut][4 * g + j], gbase + (uint32_t)row) : 0ull;
-          }
-          uint64_t* p = dst + 8 * g + 4 * h;
-          st128(p, u32x4{(uint32_t)kk[0], (uint32_t)(kk[0] >> 32), (uint32_t)kk[1],
-                         (uint32_t)(kk[1] >> 32)});
-          st128(p + 2, u32x4{(uint32_t)kk[2], (uint32_t)(kk[2] >> 32), (uint32_t)kk[3],
-                             (uint32_t)(kk[3] >> 32)});
-          vmc += 2;
-        }
-      }
-      if (t == WARM - 1 || t == ntiles - 1) {
-        const int n_in = (t + 1) * kTileItems;
-        for (int s = lane; s < UPW; s += 64) ucnt[s] = (uint32_t)n_in;
-        wave_lds_sync();
-#pragma unroll
-        for (int ut = 0; ut < NU_T; ++ut)
-          for (int c = 0; c < 32; ++c) compact(ut, c, n_in);
-      }
-    };
-
     // Hot test (branch-free): per user tile, a 16-way max against the threshold.
     auto any_hits = [&](f32x16 (&acc)[NU_T]) -> uint32_t {
       uint32_t bits = 0;
@@ -513,25 +527,34 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       return bits;
     };
 
-    // Append survivors to the LDS queue: one key per lane per round.
+    // Append survivors straight to their users' candidate buffers in HBM: one
+    // key per lane per round, its slot from the user's LDS key counter. No
+    // call and no queue in the hot loop, so nothing forces the accumulators
+    // and B fragments out of registers. A stage adds at most MARGIN keys per
+    // user, so a buffer compacted at the stage end never overflows.
     auto enqueue = [&](int t, f32x16 (&acc)[NU_T], uint32_t hit_bits) {
       DG_T0(t_e);
       const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
       const int valid = (int)((i_end - tile0) < kTileItems ? (i_end - tile0) : kTileItems);
       const uint32_t gbase = (uint32_t)(a.item_base + tile0);
+      uint32_t vmask = 0xffffu;  // rows past the slice end (last tile only)
+      if (valid < kTileItems) {
+        vmask = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+          vmask |= (row < valid ? 1u : 0u) << r;
+        }
+      }
 #pragma unroll
       for (int ut = 0; ut < NU_T; ++ut) {
         if (!(hit_bits & (1u << ut))) continue;
         uint32_t mask = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-          mask |= ((acc[ut][r] > thr[ut]) && row < valid ? 1u : 0u) << r;
-        }
-        while (true) {
-          const uint64_t act = __ballot(mask != 0u);
-          if (act == 0ull) break;
-          if (qlen > kQcap - 64) drain();
+        for (int r = 0; r < 16; ++r) mask |= (acc[ut][r] > thr[ut] ? 1u : 0u) << r;
+        mask &= vmask;
+        uint64_t* ubuf = cbase + (size_t)(ut * 32 + col) * CAP;  // this lane's user buffer
+        while (__ballot(mask != 0u) != 0ull) {
           const bool has = mask != 0u;
           const int r = has ? __builtin_ctz(mask) : 0;
           mask &= mask - 1u;
@@ -539,12 +562,11 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
 #pragma unroll
           for (int q = 1; q < 16; ++q) v = (r == q) ? acc[ut][q] : v;
           const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-          const int pos = qlen + lane_prefix(act);
           if (has) {
-            qkey[pos] = dr::make_key(v, gbase + (uint32_t)row);
-            qslot[pos] = (uint32_t)(ut * 32 + col);
+            const uint32_t pos = atomicAdd(&ucnt[ut * 32 + col], 1u);
+            st64(ubuf + pos, dr::make_key(v, gbase + (uint32_t)row));
           }
-          qlen += __popcll(act);
+          vmc += 1;  // the store above issued once (some lane had a key)
         }
       }
       DG_ADD(kDgEnqueue, t_e);
@@ -579,20 +601,13 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         if (i == st) vs[i] = vmc;
     }
     auto epilogue = [&](int t, f32x16 (&acc)[NU_T]) {
-      if (t < WARM) {
-        warm_fill(t, acc);
-      } else {
-        DG_T0(t_h);
-        uint32_t hit_bits = any_hits(acc);
-        DG_ADD(kDgHits, t_h);
-        hit_bits = __builtin_amdgcn_readfirstlane(hit_bits);  // ballots: uniform
-        if (hit_bits != 0u) enqueue(t, acc, hit_bits);
-        // end of a stage: publish the survivors and compact full buffers
-        if ((t + 1) % SR == 0 || t + 1 == ntiles) {
-          if (qlen > 0) drain();
-          check_compact();
-        }
-      }
+      DG_T0(t_h);
+      uint32_t hit_bits = any_hits(acc);
+      DG_ADD(kDgHits, t_h);
+      hit_bits = __builtin_amdgcn_readfirstlane(hit_bits);  // ballots: uniform
+      if (hit_bits != 0u) enqueue(t, acc, hit_bits);
+      // end of a stage: compact the buffers that passed flush_at
+      if ((t + 1) % SR == 0 || t + 1 == ntiles) check_compact();
     };
     // One accumulator set: the partner wave on the same SIMD issues its MFMAs
     // while this wave runs the epilogue (two waves per SIMD by design).
@@ -605,7 +620,6 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       DG_ADD(kDgMma, t_m);
       epilogue(t, acc);
     }
-    if (qlen > 0) drain();
     wait_vmcnt<0>();
     wave_lds_sync();
     for (int s = lane; s < UPW; s += 64)
@@ -622,24 +636,22 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
 #endif
 }
 
-// ------------------------------------------------------------------ finalize
-// One wave per user: all chunks' candidate keys -> drop excluded items ->
-// wave-wide register bitonic sort -> k best, decoded.
+// ------------------------------------------------------------------ per-user gather
+// One user's candidate keys of every chunk into registers (element e = lane*P
+// + i), excluded items dropped; 0 = empty.
 template <int P>
-__global__ __launch_bounds__(256) void topk_finalize_kernel(
-    const uint64_t* __restrict__ cand, const int32_t* __restrict__ cnt, int n_chunks, int cap,
-    int64_t n_users, int64_t n_users_pad, int k, const int64_t* __restrict__ excl_rowptr,
-    const int32_t* __restrict__ excl_items, float* __restrict__ out_s,
-    int32_t* __restrict__ out_i) {
+__device__ __forceinline__ void gather_candidates(const uint64_t* __restrict__ cand,
+                                                  const int32_t* __restrict__ cnt, int n_chunks,
+                                                  int cap, int64_t u, int64_t n_users_pad,
+                                                  const int64_t* __restrict__ excl_rowptr,
+                                                  const int32_t* __restrict__ excl_items,
+                                                  uint64_t (&key)[P]) {
   const int lane = dr::lane_id();
-  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-  if (u >= n_users) return;  // wave-uniform
   int off[9];
   off[0] = 0;
   for (int c = 0; c < 8; ++c)
     off[c + 1] = off[c] + (c < n_chunks ? cnt[(size_t)c * n_users_pad + u] : 0);
   const int total = off[8];
-  uint64_t key[P];
 #pragma unroll
   for (int i = 0; i < P; ++i) {
     const int e = lane * P + i;
@@ -663,6 +675,22 @@ __global__ __launch_bounds__(256) void topk_finalize_kernel(
           sorted_contains(excl_items + e0, (int)(e1 - e0), (int32_t)dr::key_item(key[i])))
         key[i] = 0ull;
   }
+}
+
+// ------------------------------------------------------------------ finalize
+// One wave per user: all chunks' candidate keys -> drop excluded items ->
+// wave-wide register bitonic sort -> k best, decoded.
+template <int P>
+__global__ __launch_bounds__(256) void topk_finalize_kernel(
+    const uint64_t* __restrict__ cand, const int32_t* __restrict__ cnt, int n_chunks, int cap,
+    int64_t n_users, int64_t n_users_pad, int k, const int64_t* __restrict__ excl_rowptr,
+    const int32_t* __restrict__ excl_items, float* __restrict__ out_s,
+    int32_t* __restrict__ out_i) {
+  const int lane = dr::lane_id();
+  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (u >= n_users) return;  // wave-uniform
+  uint64_t key[P];
+  gather_candidates<P>(cand, cnt, n_chunks, cap, u, n_users_pad, excl_rowptr, excl_items, key);
   dr::wave_sort_desc<P>(key);
 #pragma unroll
   for (int i = 0; i < P; ++i) {
@@ -672,6 +700,39 @@ __global__ __launch_bounds__(256) void topk_finalize_kernel(
       out_s[u * k + e] = empty ? -INFINITY : dr::key_score(key[i]);
       out_i[u * k + e] = empty ? -1 : (int32_t)dr::key_item(key[i]);
     }
+  }
+}
+
+// ------------------------------------------------------------------ threshold
+// One wave per user position of the sample scan: the starting threshold of the
+// main scan, strictly below the user's k-th best (non-excluded) sample score,
+// so every score >= it passes the scan's `score > thr` test. -inf when the
+// sample holds fewer than k candidates; +inf for padding positions (no user).
+template <int P>
+__global__ __launch_bounds__(256) void topk_threshold_kernel(
+    const uint64_t* __restrict__ cand, const int32_t* __restrict__ cnt, int n_chunks, int cap,
+    int64_t n_users, int64_t n_users_pad, int k, const int64_t* __restrict__ excl_rowptr,
+    const int32_t* __restrict__ excl_items, float* __restrict__ thr) {
+  const int lane = dr::lane_id();
+  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (u >= n_users_pad) return;  // wave-uniform
+  if (u >= n_users) {
+    if (lane == 0) thr[u] = INFINITY;
+    return;
+  }
+  uint64_t key[P];
+  gather_candidates<P>(cand, cnt, n_chunks, cap, u, n_users_pad, excl_rowptr, excl_items, key);
+  dr::wave_sort_desc<P>(key);
+  const int e = k - 1;
+  if (lane == e / P) {
+    const uint64_t kk = dr::select_reg<P>(key, e % P);
+    float t = -INFINITY;
+    if (kk != 0ull) {
+      const float s = dr::key_score(kk);
+      const float below = s - fmaxf(fabsf(s) * 0x1p-20f, 0x1p-100f);
+      t = below < s ? below : -INFINITY;  // NaN / inf scores: no pruning
+    }
+    thr[u] = t;
   }
 }
 
@@ -739,26 +800,27 @@ int device_cus() {
   return cus > 0 ? cus : 256;
 }
 
-// Smallest candidate capacity that still has a quarter of its compaction
-// threshold free after a compaction to k + kSlack keys.
+int64_t stage_items_for(int d) { return (int64_t)(kStageBytes / (kTileItems * d * 2)) * kTileItems; }
+
+// Smallest candidate capacity that leaves at least 32 keys of headroom above
+// k + kSlack once a stage's worth of new keys (the margin) is reserved.
 int cap_for(int d, int k) {
-  const int margin = (kStageBytes / (kTileItems * d * 2)) * kTileItems;
+  const int margin = (int)stage_items_for(d);
   for (int cap = 512; cap <= 2048; cap <<= 1)
-    if ((k + kSlack) * 4 <= (cap - margin) * 3) return cap;
+    if (k + kSlack + 32 <= cap - margin) return cap;
   return -1;
 }
 
 Plan make_plan(int64_t n_users, int64_t n_items, int d, int k) {
   Plan p{};
   p.cap = cap_for(d, k);
-  const int nut = d >= 256 ? 1 : 2;
-  p.users_per_wg = nut * 32 * kWaves;
+  p.users_per_wg = nut_for(d) * 32 * kWaves;
   p.n_ublocks = dr::ceil_div(n_users, p.users_per_wg);
   p.n_users_pad = p.n_ublocks * p.users_per_wg;
   const int slots = device_cus();  // one 512-thread workgroup per CU
-  const int64_t stage_items = (kStageBytes / (kTileItems * d * 2)) * kTileItems;
+  const int64_t stage_items = stage_items_for(d);
   // Split the catalog into chunks only to balance the tail of the grid; each
-  // chunk must stay long enough to amortise its warm-up, and the finalize
+  // chunk must stay long enough to amortise its start, and the finalize
   // kernel sorts at most 2048 candidates per user.
   const int64_t min_chunk = 65536;
   int best_s = 1;
@@ -783,13 +845,76 @@ Plan make_plan(int64_t n_users, int64_t n_items, int d, int k) {
   return p;
 }
 
-size_t diag_bytes(const Plan& p) {
-#ifdef DR_TOPK_DIAG
-  return (size_t)p.grid * kWaves * kDgSlots * sizeof(uint64_t);
+// Items of the threshold sample (the slice's first S rows), 0 = no pre-pass.
+int64_t sample_items(int64_t n_items, int d) {
+#if DR_PREPASS
+  constexpr int64_t kMinItems = 1 << 18;  // smaller catalogs scan once, unseeded
+  if (n_items < kMinItems) return 0;
+  int64_t s = n_items / 64;
+  s = s < 65536 ? s : 65536;
+  const int64_t st = stage_items_for(d);
+  return dr::ceil_div(s, st) * st;
 #else
-  (void)p;
+  (void)n_items;
+  (void)d;
   return 0;
 #endif
+}
+
+size_t diag_bytes() {
+#ifdef DR_TOPK_DIAG
+  return (size_t)device_cus() * kWaves * kDgSlots * sizeof(uint64_t);
+#else
+  return 0;
+#endif
+}
+
+// Workspace layout: [cand | cnt | thr | diag], 256-B aligned pieces. The
+// sample scan and the main scan run one after the other on the stream and
+// share the candidate region.
+struct Layout {
+  Plan main, sample;
+  int64_t S;
+  size_t cand, cnt, thr, diag;
+  size_t total() const { return cand + cnt + thr + diag; }
+};
+
+Layout make_layout(int64_t n_users, int64_t n_items, int d, int k) {
+  Layout L{};
+  L.main = make_plan(n_users, n_items, d, k);
+  L.S = sample_items(n_items, d);
+  L.cand = L.main.cand_bytes;
+  L.cnt = L.main.cnt_bytes;
+  if (L.S > 0) {
+    L.sample = make_plan(n_users, L.S, d, k);
+    L.cand = L.cand > L.sample.cand_bytes ? L.cand : L.sample.cand_bytes;
+    L.cnt = L.cnt > L.sample.cnt_bytes ? L.cnt : L.sample.cnt_bytes;
+    L.thr = ((size_t)L.main.n_users_pad * sizeof(float) + 255) & ~(size_t)255;
+  }
+  L.diag = diag_bytes();
+  return L;
+}
+
+template <bool SEEDED>
+void launch_scan(const Plan& p, const TopkArgs& a, int d, hipStream_t s) {
+#define DR_SCAN(DD, CC) \
+  hipLaunchKernelGGL((score_scan_kernel<DD, CC, SEEDED>), dim3(p.grid), dim3(kThreads), 0, s, a)
+#define DR_SCAN_D(CC)                  \
+  switch (d) {                         \
+    case 32: DR_SCAN(32, CC); break;   \
+    case 64: DR_SCAN(64, CC); break;   \
+    case 128: DR_SCAN(128, CC); break; \
+    default: DR_SCAN(256, CC); break;  \
+  }
+  if (p.cap == 512) {
+    DR_SCAN_D(512)
+  } else if (p.cap == 1024) {
+    DR_SCAN_D(1024)
+  } else {
+    DR_SCAN_D(2048)
+  }
+#undef DR_SCAN_D
+#undef DR_SCAN
 }
 
 }  // namespace
@@ -798,18 +923,17 @@ extern "C" size_t dr_score_topk_workspace(int64_t n_users, int64_t n_items, int 
   if (n_users <= 0 || n_items <= 0 || k <= 0) return 0;
   if (d != 32 && d != 64 && d != 128 && d != 256) return 0;
   if (cap_for(d, k) < 0) return 0;
-  Plan p = make_plan(n_users, n_items, d, k);
-  return p.cand_bytes + p.cnt_bytes + diag_bytes(p) + 256;
+  return make_layout(n_users, n_items, d, k).total() + 256;
 }
 
 #ifdef DR_TOPK_DIAG
 // Diag builds only: byte offset (from the 256-B aligned workspace base) of the
-// [grid*8][16] u64 counter block, and the grid size.
+// [grid*8][16] u64 counter block of the main scan, and its grid size.
 extern "C" size_t dr_score_topk_diag_offset(int64_t n_users, int64_t n_items, int d, int k,
                                             int* grid) {
-  Plan p = make_plan(n_users, n_items, d, k);
-  *grid = p.grid;
-  return p.cand_bytes + p.cnt_bytes;
+  Layout L = make_layout(n_users, n_items, d, k);
+  *grid = L.main.grid;
+  return L.cand + L.cnt + L.thr;
 }
 #endif
 
@@ -835,14 +959,15 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   }
   DR_CHECK_ARG(item_table, "null item_table");
   hipStream_t s = (hipStream_t)stream;
-  Plan p = make_plan(n_users, n_items, d, k);
-  const size_t need = p.cand_bytes + p.cnt_bytes + diag_bytes(p);
+  const Layout L = make_layout(n_users, n_items, d, k);
+  const size_t need = L.total();
   char* ws = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
   if (!workspace || (size_t)(ws - (char*)workspace) + need > workspace_bytes) {
     dr::set_error("dr_score_topk: workspace too small (need " + std::to_string(need + 256) +
                   " bytes)");
     return DR_EWORKSPACE;
   }
+  const Plan& p = L.main;
   TopkArgs a;
   a.U = (const __bf16*)user_table;
   a.user_ids = user_ids;
@@ -857,45 +982,53 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   a.n_chunks = p.n_chunks;
   a.chunk_items = p.chunk_items;
   a.n_ublocks = p.n_ublocks;
+  a.init_thr = nullptr;
   a.cand = (uint64_t*)ws;
-  a.cnt = (int32_t*)(ws + p.cand_bytes);
-  a.diag = (uint64_t*)(ws + p.cand_bytes + p.cnt_bytes);  // written only in DIAG builds
+  a.cnt = (int32_t*)(ws + L.cand);
+  a.diag = (uint64_t*)(ws + L.cand + L.cnt + L.thr);  // written only in DIAG builds
+  const int fin_grid = (int)dr::ceil_div(n_users, 4);
 
-#define DR_SCAN(DD, CC) \
-  hipLaunchKernelGGL((score_scan_kernel<DD, CC>), dim3(p.grid), dim3(kThreads), 0, s, a)
-#define DR_SCAN_D(CC)                  \
-  switch (d) {                         \
-    case 32: DR_SCAN(32, CC); break;   \
-    case 64: DR_SCAN(64, CC); break;   \
-    case 128: DR_SCAN(128, CC); break; \
-    default: DR_SCAN(256, CC); break;  \
+#define DR_BY_P(PP_EXPR, LAUNCH)                                           \
+  switch (PP_EXPR) {                                                       \
+    case 8: LAUNCH(8); break;                                              \
+    case 16: LAUNCH(16); break;                                            \
+    case 32: LAUNCH(32); break;                                            \
+    default:                                                               \
+      dr::set_error("dr_score_topk: internal plan error (candidate sort)"); \
+      return DR_EUNSUPPORTED;                                              \
   }
-  if (p.cap == 512) {
-    DR_SCAN_D(512)
-  } else if (p.cap == 1024) {
-    DR_SCAN_D(1024)
+
+  if (L.S > 0) {
+    // Pre-pass: unseeded scan of the first S items, then per-user thresholds.
+    TopkArgs as = a;
+    as.n_items = L.S;
+    as.n_chunks = L.sample.n_chunks;
+    as.chunk_items = L.sample.chunk_items;
+    launch_scan<false>(L.sample, as, d, s);
+    DR_CHECK_LAUNCH();
+    float* thr = (float*)(ws + L.cand + L.cnt);
+    const int thr_grid = (int)dr::ceil_div(p.n_users_pad, 4);
+#define DR_THR(PP)                                                                              \
+  hipLaunchKernelGGL((topk_threshold_kernel<PP>), dim3(thr_grid), dim3(256), 0, s, a.cand,       \
+                     a.cnt, L.sample.n_chunks, L.sample.cap, n_users, p.n_users_pad, k,           \
+                     excl_rowptr, excl_items, thr)
+    DR_BY_P(p_for(L.sample.n_chunks * L.sample.cap), DR_THR)
+#undef DR_THR
+    DR_CHECK_LAUNCH();
+    a.init_thr = thr;
+    launch_scan<true>(p, a, d, s);
   } else {
-    DR_SCAN_D(2048)
+    launch_scan<false>(p, a, d, s);
   }
-#undef DR_SCAN_D
-#undef DR_SCAN
   DR_CHECK_LAUNCH();
 
-  const int P = p_for(p.n_chunks * p.cap);
-  const int grid = (int)dr::ceil_div(n_users, 4);
-#define DR_FIN(PP)                                                                            \
-  hipLaunchKernelGGL((topk_finalize_kernel<PP>), dim3(grid), dim3(256), 0, s, a.cand, a.cnt,  \
-                     p.n_chunks, p.cap, n_users, p.n_users_pad, k, excl_rowptr, excl_items,   \
+#define DR_FIN(PP)                                                                             \
+  hipLaunchKernelGGL((topk_finalize_kernel<PP>), dim3(fin_grid), dim3(256), 0, s, a.cand, a.cnt, \
+                     p.n_chunks, p.cap, n_users, p.n_users_pad, k, excl_rowptr, excl_items,     \
                      out_scores, out_items)
-  switch (P) {
-    case 8: DR_FIN(8); break;
-    case 16: DR_FIN(16); break;
-    case 32: DR_FIN(32); break;
-    default:
-      dr::set_error("dr_score_topk: internal plan error (finalize size)");
-      return DR_EUNSUPPORTED;
-  }
+  DR_BY_P(p_for(p.n_chunks * p.cap), DR_FIN)
 #undef DR_FIN
+#undef DR_BY_P
   DR_CHECK_LAUNCH();
   return DR_OK;
 }
