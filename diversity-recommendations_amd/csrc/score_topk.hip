@@ -62,7 +62,7 @@ using dr::f32x16;
 #endif
 enum {
   kDgTotal, kDgPrologue, kDgBoundary, kDgMma, kDgHits, kDgEnqueue, kDgDrain, kDgFlush,
-  kDgNTiles, kDgNEnqueue, kDgNDrain, kDgNFlush, kDgNStages, kDgSlots = 16
+  kDgNTiles, kDgNEnqueue, kDgNDrain, kDgNFlush, kDgNStages, kDgRealtime, kDgSlots = 16
 };
 
 // Geometry knobs. The defaults are the product configuration; the -D
@@ -399,6 +399,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
 #ifdef DR_TOPK_DIAG
   uint64_t dg[kDgSlots] = {};
   DG_T0(t_kernel);
+  const uint64_t rt_kernel = __builtin_amdgcn_s_memrealtime();  // 100 MHz: clock = cycles / time
 #endif
   const int64_t n_units = a.n_ublocks * a.n_chunks;
   for (int64_t unit = blockIdx.x; unit < n_units; unit += gridDim.x) {
@@ -628,6 +629,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
   }
 #ifdef DR_TOPK_DIAG
   DG_ADD(kDgTotal, t_kernel);
+  dg[kDgRealtime] = __builtin_amdgcn_s_memrealtime() - rt_kernel;
   if (lane == 0) {
     uint64_t* o = a.diag + ((size_t)blockIdx.x * kWaves + wave) * kDgSlots;
 #pragma unroll
@@ -635,6 +637,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
   }
 #endif
 }
+
 
 // ------------------------------------------------------------------ per-user gather
 // One user's candidate keys of every chunk into registers (element e = lane*P

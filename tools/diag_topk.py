@@ -23,7 +23,7 @@ import torch  # noqa: E402
 from divrec import _backend as B  # noqa: E402
 
 SLOTS = ["total", "prologue", "boundary", "mma_issue", "hits", "enqueue", "drain", "flush",
-         "n_tiles", "n_enqueue", "n_drain", "n_flush", "n_stages"]
+         "n_tiles", "n_enqueue", "n_drain", "n_flush", "n_stages", "realtime_100mhz"]
 
 
 def main():
@@ -71,6 +71,8 @@ def main():
     res["shares"] = {nm: round(res[nm] / cyc, 4) for nm in SLOTS[1:8]}
     res["tflops"] = 2.0 * args.users * args.items * args.dim / (ms * 1e-3) / 1e12
     res["cycles_per_tile"] = cyc / max(1, res["n_tiles"])
+    # in-kernel shader clock: s_memtime cycles / s_memrealtime ticks (100 MHz)
+    res["clock_ghz"] = cyc / max(1.0, res["realtime_100mhz"]) * 0.1
     print(json.dumps(res))
 
 
