@@ -18,6 +18,13 @@ time of the call on its stream); `traffic` comes from a committed rocprofv3 PMC
 summary (profiles/pmc_traffic.json) when one exists for this exact config.
 `cpu_baseline` (N=1 only) times the CPU oracle — the reference algorithm,
 restated — on a bounded user sample on this host.
+
+Secondary workloads (single GPU, one JSON line each, same schema; the driver
+runs the default only): ``--workload score1m`` (BASELINE configs[1]: 1M x 1M,
+d=64, top-100), ``gather`` (the MatrixFactorization.forward row gather on
+1M x 1M fp32 tables, HBM roofline), ``bpr`` (configs[2]: one BPR training step
+= fused gather + loss + gradient scatter + dense Adam over both tables) and
+``mmr`` (configs[4]: MMR re-rank of 1000 candidates to 100 per user).
 """
 from __future__ import annotations
 
@@ -52,6 +59,8 @@ def parse():
     ap.add_argument("--ild-kind", default="cosine")
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="catalog",
+                    choices=["catalog", "score1m", "gather", "bpr", "mmr"])
     return ap.parse_args()
 
 
@@ -120,6 +129,8 @@ def load_traffic(cfg_key: str):
 
 def main():
     args = parse()
+    if args.workload != "catalog":
+        return secondary(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -223,6 +234,196 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- secondary workloads
+def _timed(fn, steps: int, warmup: int):
+    """Run fn() warmup + steps times; return (wall seconds per step, device
+    seconds per step from HIP events on the current stream)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(steps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps, e0.elapsed_time(e1) / 1e3 / steps
+
+
+def _line(metric, value, unit, args, step_s, dtype, config, roofline, cpu, **extra):
+    rec = {"metric": metric, "value": value, "unit": unit, "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True,
+           "scaling": "replicas", "vs_baseline": None, "dtype": dtype,
+           "data": "synthetic (seeded)", "config": config, "roofline": roofline,
+           "cpu_baseline": cpu}
+    rec.update(extra)
+    print(json.dumps(rec), flush=True)
+
+
+def _hbm(bytes_per_launch, seconds, traffic=None):
+    gbs = bytes_per_launch / seconds / 1e9
+    return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_launch": bytes_per_launch}
+
+
+def secondary(args):
+    import numpy as np
+
+    sys.path.insert(0, ROOT)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(1234)
+    want_cpu = not args.no_cpu_baseline
+
+    if args.workload == "score1m":
+        U_n, I_n, d, k = 1_000_000, 1_000_000, 64, 100
+        users, items = gen_table(U_n, d, 1, dev), gen_table(I_n, d, 2, dev)
+        wall, dt = _timed(lambda: ops.score_topk(users, items, k), args.steps, args.warmup)
+        flops = 2.0 * U_n * I_n * d
+        cpu = None
+        if want_cpu:
+            import oracle
+
+            Uh, Ih = users[:8].float().cpu().numpy(), items.float().cpu().numpy()
+            t0 = time.perf_counter()
+            oracle.recommend_topk(Uh, Ih, k, users=list(range(8)))
+            t = time.perf_counter() - t0
+            cpu = {"value": 8 * I_n / t, "unit": "scored pairs/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle.recommend_topk, 8 users x {I_n} items, {t:.1f}s"}
+        _line("scored pairs/sec, 1M x 1M d=64 top-100 (BASELINE configs[1])", U_n * I_n / wall,
+              "scored pairs/s", args, wall, "bf16",
+              {"workload": "score_topk 1M users x 1M items d=64 k=100", "users": U_n,
+               "items": I_n, "dim": d, "k": k},
+              {"bound": "mfma", "achieved": flops / dt / 1e12, "peak": MFMA_BF16_PEAK_TFLOPS,
+               "unit": "TFLOP/s", "frac": flops / dt / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+               "traffic": None, "kernel": "dr_score_topk"}, cpu)
+        return 0
+
+    if args.workload == "gather":
+        U_n, I_n, d, n = 1_000_000, 1_000_000, 128, 1 << 23
+        Ut = torch.randn(U_n, d, generator=g, device=dev)
+        It = torch.randn(I_n, d, generator=g, device=dev)
+        uid = torch.randint(0, U_n, (n,), generator=g, device=dev)
+        iid = torch.randint(0, I_n, (n,), generator=g, device=dev)
+        wall, dt = _timed(lambda: ops.gather_dot(Ut, It, uid, iid), args.steps, args.warmup)
+        per_pair = 2 * d * 4 + 2 * 8 + 4
+        cpu = None
+        if want_cpu:
+            import oracle
+
+            Uh, Ih = Ut.cpu().numpy(), It.cpu().numpy()
+            m = 1 << 20
+            uh, ih = uid[:m].cpu().numpy(), iid[:m].cpu().numpy()
+            t0 = time.perf_counter()
+            oracle.mf_forward(Uh, Ih, uh, ih)
+            t = time.perf_counter() - t0
+            cpu = {"value": m / t, "unit": "pairs/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle.mf_forward (numpy gather + fp32 row sum), {m} pairs, {t:.2f}s"}
+        _line("MatrixFactorization.forward gathered pairs/sec (fp32 1M x 1M d=128)", n / wall,
+              "pairs/s", args, wall, "f32",
+              {"workload": f"dr_gather_dot, {n} uniform random (user, item) pairs, fp32 tables "
+                           f"{U_n}x{d} and {I_n}x{d}", "pairs": n, "dim": d},
+              dict(_hbm(per_pair * n, dt), kernel="dr_gather_dot",
+                   per_unit=f"{per_pair} B/pair = 2 rows x {d} x 4 B + 2 ids x 8 B + 4 B out"),
+              cpu)
+        return 0
+
+    if args.workload == "bpr":
+        U_n, I_n, d, B, npos = 1_000_000, 1_000_000, 128, 1 << 20, 100
+        Ut = (torch.randn(U_n, d, generator=g, device=dev) * 0.1).contiguous()
+        It = (torch.randn(I_n, d, generator=g, device=dev) * 0.1).contiguous()
+        pos = torch.sort(torch.randint(0, I_n, (U_n, npos), generator=g, device=dev), dim=1).values
+        uid = torch.randint(0, U_n, (B,), generator=g, device=dev)
+        pid = pos[uid, torch.randint(0, npos, (B,), generator=g, device=dev)]
+        nid = torch.randint(0, I_n, (B,), generator=g, device=dev)
+        clash = (pos[uid] == nid[:, None]).any(dim=1)  # reject negatives that are positives
+        nid[clash] = (nid[clash] + 1) % I_n
+        gU, gI = torch.zeros_like(Ut), torch.zeros_like(It)
+        state = [(torch.zeros_like(Ut), torch.zeros_like(Ut)), (torch.zeros_like(It), torch.zeros_like(It))]
+        step_no = [0]
+        ev = {"bpr": [], "adam": []}
+
+        def step():
+            step_no[0] += 1
+            gU.zero_()
+            gI.zero_()
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record()
+            ops.bpr_fwd_bwd(Ut, It, uid, pid, nid, 1.0 / B, gU, gI)
+            e[1].record()
+            for p_, g_, (m_, v_) in ((Ut, gU, state[0]), (It, gI, state[1])):
+                ops.adam_dense(p_, g_, m_, v_, 1e-3, 0.9, 0.999, 1e-8, 0.0, step_no[0])
+            e[2].record()
+            ev["bpr"].append((e[0], e[1]))
+            ev["adam"].append((e[1], e[2]))
+
+        wall, dt = _timed(step, args.steps, args.warmup)
+        tb = sum(a.elapsed_time(b) for a, b in ev["bpr"][-args.steps:]) / 1e3 / args.steps
+        ta = sum(a.elapsed_time(b) for a, b in ev["adam"][-args.steps:]) / 1e3 / args.steps
+        per_triple = 3 * d * 4 + 3 * 8 + 4 + 4 + 3 * d * 4  # rows + ids + loss/hit + grad adds
+        adam_bytes = 2 * (U_n + I_n) * d * 4 * 3 + (U_n + I_n) * d * 4  # p,m,v rw + g read
+        cpu = None
+        if want_cpu:
+            import oracle
+
+            m = 8192
+            Uh, Ih = Ut.cpu().numpy(), It.cpu().numpy()
+            sl = [t_[:m].cpu().numpy() for t_ in (uid, pid, nid)]
+            t0 = time.perf_counter()
+            oracle.bpr_forward_backward(Uh, Ih, *sl)
+            t_fb = time.perf_counter() - t0
+            n_adam = 1 << 22
+            p0 = Uh.reshape(-1)[:n_adam]
+            t0 = time.perf_counter()
+            oracle.adam_step(p0, p0, np.zeros_like(p0), np.zeros_like(p0), 1)
+            t_adam = (time.perf_counter() - t0) * (2 * U_n * d) / n_adam
+            cpu_step = t_fb * B / m + t_adam
+            cpu = {"value": B / cpu_step, "unit": "triples/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle.bpr_forward_backward on {m} triples ({t_fb:.2f}s, x{B // m}) + "
+                             f"oracle.adam_step on {n_adam} of {2 * U_n * d} params "
+                             f"(extrapolated {t_adam:.1f}s): {cpu_step:.0f}s per step"}
+        _line("BPR training triples/sec, 1M x 1M d=128 (BASELINE configs[2])", B / wall,
+              "triples/s", args, wall, "f32",
+              {"workload": f"one BPR step: dr_bpr_fwd_bwd over {B} triples (uniform user, "
+                           f"positive from a {npos}-item/user CSR, uniform negative) + "
+                           f"dr_adam_dense over both fp32 tables", "users": U_n, "items": I_n,
+               "dim": d, "batch": B},
+              dict(_hbm(per_triple * B, tb), kernel="dr_bpr_fwd_bwd",
+                   per_unit=f"{per_triple} B/triple"),
+              cpu, bpr_ms=tb * 1e3, adam_ms=ta * 1e3,
+              adam_roofline=_hbm(adam_bytes, ta))
+        return 0
+
+    if args.workload == "mmr":
+        U_n, I_n, d, C, kout, lam = 1_000_000, 10_000_000, 128, 1000, 100, 0.5
+        items = gen_table(I_n, d, 2, dev)
+        cand = torch.randint(0, I_n, (U_n, C), generator=g, device=dev, dtype=torch.int32)
+        sc = torch.sort(torch.rand(U_n, C, generator=g, device=dev), dim=1, descending=True).values
+        wall, dt = _timed(lambda: ops.mmr_rerank(cand, sc, items, kout, lam), args.steps,
+                          args.warmup)
+        per_user = C * d * 2 + C * 8 + kout * 4
+        cpu = None
+        if want_cpu:
+            import oracle
+
+            m = 4
+            Eh = items.float().cpu().numpy()
+            t0 = time.perf_counter()
+            oracle.mmr_greedy(cand[:m].cpu().numpy(), sc[:m].cpu().numpy(), Eh, kout, lam)
+            t = time.perf_counter() - t0
+            cpu = {"value": m / t, "unit": "users/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle.mmr_greedy (float64 numpy), {m} users, {t:.2f}s"}
+        _line("MMR re-rank users/sec, top-1000 -> top-100, d=128 (BASELINE configs[4])",
+              U_n / wall, "users/s", args, wall, "bf16",
+              {"workload": f"dr_mmr_rerank: {U_n} users x {C} candidates -> {kout}, "
+                           f"lambda={lam}, item table {I_n}x{d} bf16", "users": U_n, "dim": d},
+              dict(_hbm(per_user * U_n, dt), kernel="dr_mmr_rerank",
+                   per_unit=f"{per_user} B/user"), cpu)
+        return 0
+    raise ValueError(args.workload)
 
 
 if __name__ == "__main__":

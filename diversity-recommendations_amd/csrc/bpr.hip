@@ -6,7 +6,12 @@
 //
 // bpr_fwd_bwd is HBM/atomic-bound: per triple it reads three fp32 rows
 // (3*d*4 B), 24 B of ids, writes loss/hit, and adds 3*d*4 B of gradient with
-// fp32 atomics. A group of G lanes (16 B per lane) owns one triple.
+// fp32 atomics. A group of 32 lanes owns one triple and lane l handles row
+// elements l, l+32, l+64, ...: every load and every atomic wave-instruction
+// then covers two contiguous 128-B row segments, the shape at which
+// global_atomic_add_f32 runs at its full rate (MI355X_MICROARCH.md, Global
+// float atomics); 16-B-per-lane chunks would scatter each atomic instruction
+// over 16-B strides. Any d <= 512.
 #include <cmath>
 
 #include "common.h"
@@ -28,35 +33,37 @@ __device__ __forceinline__ float neg_log_sigmoid_grad(float x) {
   return -(x >= 0.f ? e / (1.f + e) : 1.f / (1.f + e));
 }
 
-template <int G, int CH>
+template <int E>  // row elements per lane: ceil(d / 32)
 __global__ __launch_bounds__(kBlock) void bpr_kernel(
     const float* __restrict__ U, const float* __restrict__ I, int64_t d,
     const int64_t* __restrict__ uid, const int64_t* __restrict__ pid,
     const int64_t* __restrict__ nid, int64_t batch, float grad_scale, float* __restrict__ loss,
     int32_t* __restrict__ hit, float* __restrict__ gU, float* __restrict__ gI) {
-  const int gl = threadIdx.x % G;
-  const int64_t group = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / G;
-  const int64_t ngroups = (int64_t)gridDim.x * kBlock / G;
+  const int gl = threadIdx.x & 31;
+  const int64_t group = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 5;
+  const int64_t ngroups = (int64_t)gridDim.x * kBlock / 32;
   for (int64_t b = group; b < batch; b += ngroups) {
     const int64_t u = uid[b], p = pid[b], n = nid[b];
-    float4 uv[CH], pv[CH], nv[CH];
+    const float* ur = U + u * d;
+    const float* pr = I + p * d;
+    const float* nr = I + n * d;
+    float uv[E], pv[E], nv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t x = e * 32 + gl;
+      const bool ok = x < d;
+      uv[e] = ok ? ur[x] : 0.f;
+      pv[e] = ok ? pr[x] : 0.f;
+      nv[e] = ok ? nr[x] : 0.f;
+    }
     float sp = 0.f, sn = 0.f;
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int64_t off = (int64_t)(c * G + gl) * 4;
-      uv[c] = ld4(U + u * d + off);
-      pv[c] = ld4(I + p * d + off);
-      nv[c] = ld4(I + n * d + off);
+    for (int e = 0; e < E; ++e) {
+      sp = fmaf(uv[e], pv[e], sp);
+      sn = fmaf(uv[e], nv[e], sn);
     }
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      sp = fmaf(uv[c].x, pv[c].x, sp); sp = fmaf(uv[c].y, pv[c].y, sp);
-      sp = fmaf(uv[c].z, pv[c].z, sp); sp = fmaf(uv[c].w, pv[c].w, sp);
-      sn = fmaf(uv[c].x, nv[c].x, sn); sn = fmaf(uv[c].y, nv[c].y, sn);
-      sn = fmaf(uv[c].z, nv[c].z, sn); sn = fmaf(uv[c].w, nv[c].w, sn);
-    }
-#pragma unroll
-    for (int m = G / 2; m > 0; m >>= 1) {
+    for (int m = 16; m > 0; m >>= 1) {  // xor < 32 stays inside the 32-lane group
       sp += __shfl_xor(sp, m);
       sn += __shfl_xor(sn, m);
     }
@@ -66,24 +73,14 @@ __global__ __launch_bounds__(kBlock) void bpr_kernel(
       if (hit) hit[b] = sp >= sn ? 1 : 0;
     }
     const float g = neg_log_sigmoid_grad(x) * grad_scale;
-    if (gU || gI) {
 #pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        const int64_t off = (int64_t)(c * G + gl) * 4;
-        if (gU) {
-          float* o = gU + u * d + off;
-          atomicAdd(o + 0, g * pv[c].x - g * nv[c].x);
-          atomicAdd(o + 1, g * pv[c].y - g * nv[c].y);
-          atomicAdd(o + 2, g * pv[c].z - g * nv[c].z);
-          atomicAdd(o + 3, g * pv[c].w - g * nv[c].w);
-        }
+    for (int e = 0; e < E; ++e) {
+      const int64_t x2 = e * 32 + gl;
+      if (x2 < d) {
+        if (gU) atomicAdd(gU + u * d + x2, g * pv[e] - g * nv[e]);
         if (gI) {
-          float* op = gI + p * d + off;
-          float* on = gI + n * d + off;
-          atomicAdd(op + 0, g * uv[c].x); atomicAdd(op + 1, g * uv[c].y);
-          atomicAdd(op + 2, g * uv[c].z); atomicAdd(op + 3, g * uv[c].w);
-          atomicAdd(on + 0, -g * uv[c].x); atomicAdd(on + 1, -g * uv[c].y);
-          atomicAdd(on + 2, -g * uv[c].z); atomicAdd(on + 3, -g * uv[c].w);
+          atomicAdd(gI + p * d + x2, g * uv[e]);
+          atomicAdd(gI + n * d + x2, -g * uv[e]);
         }
       }
     }
@@ -127,27 +124,27 @@ extern "C" int dr_bpr_fwd_bwd(const float* user_table, const float* item_table, 
   DR_CHECK_ARG(batch >= 0, "batch must be >= 0");
   if (batch == 0) return DR_OK;
   DR_CHECK_ARG(user_table && item_table && user_id && pos_id && neg_id, "null pointer");
-  DR_CHECK_ARG(d % 4 == 0 && d >= 16 && d <= 512, "d must be a multiple of 4 in [16, 512]");
+  DR_CHECK_ARG(d >= 1 && d <= 512, "d must be in [1, 512]");
   hipStream_t s = (hipStream_t)stream;
-  const int64_t chunks = d / 4;  // 16-B chunks per row
-  auto go = [&](auto kern, int G) {
-    int64_t grid = dr::ceil_div(batch, kBlock / G);
-    if (grid > 256 * 8) grid = 256 * 8;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, s, user_table, item_table,
-                       d, user_id, pos_id, neg_id, batch, grad_scale, loss, hit, grad_user,
-                       grad_item);
-  };
-  switch (chunks) {
-    case 4: go(bpr_kernel<4, 1>, 4); break;
-    case 8: go(bpr_kernel<8, 1>, 8); break;
-    case 16: go(bpr_kernel<16, 1>, 16); break;
-    case 32: go(bpr_kernel<32, 1>, 32); break;
-    case 64: go(bpr_kernel<64, 1>, 64); break;
-    case 128: go(bpr_kernel<64, 2>, 64); break;
-    default:
-      dr::set_error("dr_bpr_fwd_bwd: d/4 must be a power of two in [4, 128]");
-      return DR_EUNSUPPORTED;
+  int64_t grid = dr::ceil_div(batch, kBlock / 32);
+  if (grid > 256 * 8) grid = 256 * 8;  // grid-stride the rest
+#define DR_BPR(EE)                                                                          \
+  hipLaunchKernelGGL(bpr_kernel<EE>, dim3((unsigned)grid), dim3(kBlock), 0, s, user_table,  \
+                     item_table, d, user_id, pos_id, neg_id, batch, grad_scale, loss, hit,   \
+                     grad_user, grad_item)
+  switch ((int)dr::ceil_div(d, 32)) {
+    case 1: DR_BPR(1); break;
+    case 2: DR_BPR(2); break;
+    case 3: DR_BPR(3); break;
+    case 4: DR_BPR(4); break;
+    case 5: DR_BPR(5); break;
+    case 6: DR_BPR(6); break;
+    case 7: DR_BPR(7); break;
+    case 8: DR_BPR(8); break;
+    case 9: case 10: case 11: case 12: DR_BPR(12); break;
+    default: DR_BPR(16); break;
   }
+#undef DR_BPR
   DR_CHECK_LAUNCH();
   return DR_OK;
 }

@@ -183,25 +183,26 @@ __global__ __launch_bounds__(256) void ild_embedding_kernel(const R* __restrict_
 }
 
 // Register-resident variant for nt = NT row tiles: every row of the list is
-// gathered into MFMA fragments up front (all loads in flight together, one
-// HBM round trip per user instead of one per tile pair), then the norms and
-// the upper-triangle Gram tiles are formed from registers. Same summation
-// order as ild_embedding_kernel. Fragments: NT * D/16 * 4 VGPRs (128 at
-// NT=4, D=128).
-template <typename R, int D, int NT>
+// gathered into MFMA fragments up front (all loads in flight together), then
+// the norms and the upper-triangle Gram tiles are formed from registers. The
+// per-row terms (|e|^2, and 1/|e| for cosine) are computed once per row, so a
+// pair costs one fma (cosine), nothing (dot) or one sqrt (euclidean); the
+// pair mask is structural (off-diagonal tiles need only j < k). Fragments:
+// NT * D/16 * 4 VGPRs (128 at NT=4, D=128).
+template <typename R, int D, int NT, int KIND>
 __global__ __launch_bounds__(256) void ild_embedding_regs(const R* __restrict__ recs,
                                                           int64_t n_users, int k,
                                                           const __bf16* __restrict__ E,
-                                                          int kind, float* __restrict__ out) {
+                                                          float* __restrict__ out) {
   constexpr int KS = D / 16;
-  __shared__ float s_nsq[4][NT * 32];
+  __shared__ float s_w[4][NT * 32];  // per row: 1/|e| (cosine) or |e|^2 (euclidean)
   const int lane = dr::lane_id();
   const int wave = threadIdx.x >> 6;
   const int h = lane >> 5, col = lane & 31;
   const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   if (u >= n_users) return;  // wave-uniform
   const R* r = recs + u * k;
-  float* nsq = s_nsq[wave];
+  float* w = s_w[wave];
   bf16x8 x[NT][KS];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -211,37 +212,44 @@ __global__ __launch_bounds__(256) void ild_embedding_regs(const R* __restrict__ 
 #pragma unroll
     for (int s = 0; s < KS; ++s) x[t][s] = __builtin_bit_cast(bf16x8, src[2 * s]);
   }
+  if constexpr (KIND != DR_ILD_DOT) {
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const f32x16 g = gram_tile<D>(x[t], x[t]);
-    const int ri = (col & 3) + 4 * (col >> 3);
-    float v = g[0];
+    for (int t = 0; t < NT; ++t) {
+      const f32x16 g = gram_tile<D>(x[t], x[t]);
+      const int ri = (col & 3) + 4 * (col >> 3);
+      float v = g[0];
 #pragma unroll
-    for (int q = 1; q < 16; ++q) v = (ri == q) ? g[q] : v;
-    if (((col >> 2) & 1) == h) nsq[32 * t + col] = v;
+      for (int q = 1; q < 16; ++q) v = (ri == q) ? g[q] : v;
+      if (KIND == DR_ILD_COSINE) v = 1.f / sqrtf(v);
+      if (((col >> 2) & 1) == h) w[32 * t + col] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   float sum = 0.f;
 #pragma unroll
   for (int ti = 0; ti < NT; ++ti) {
+    float wi[16];
+    if constexpr (KIND != DR_ILD_DOT) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) wi[q] = w[32 * ti + (q & 3) + 8 * (q >> 2) + 4 * h];
+    }
 #pragma unroll
     for (int tj = ti; tj < NT; ++tj) {
       const f32x16 g = gram_tile<D>(x[ti], x[tj]);
       const int j = 32 * tj + col;
-      const float nj = j < k ? nsq[j] : 1.f;
+      const bool jv = j < k;
+      const float wj = (KIND != DR_ILD_DOT && jv) ? w[j] : 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int i = 32 * ti + (q & 3) + 8 * (q >> 2) + 4 * h;
-        if (i < j && j < k) {
-          const float ni = nsq[i];
-          float dist;
-          if (kind == DR_ILD_COSINE) dist = 1.f - g[q] / (sqrtf(ni) * sqrtf(nj));
-          else if (kind == DR_ILD_DOT) dist = g[q];
-          else dist = sqrtf(fmaxf(ni + nj - 2.f * g[q], 0.f));
-          sum += dist;
-        }
+        const bool ok = jv && (ti < tj || i < j);
+        float dist;
+        if constexpr (KIND == DR_ILD_COSINE) dist = fmaf(-g[q], wi[q] * wj, 1.f);
+        else if constexpr (KIND == DR_ILD_DOT) dist = g[q];
+        else dist = sqrtf(fmaxf(wi[q] + wj - 2.f * g[q], 0.f));
+        sum += ok ? dist : 0.f;
       }
     }
   }
@@ -249,15 +257,23 @@ __global__ __launch_bounds__(256) void ild_embedding_regs(const R* __restrict__ 
   if (lane == 0) out[u] = sum / (float)(k * (k - 1));
 }
 
+template <typename R, int D, int KIND>
+void launch_regs_kind(const R* recs, int64_t n_users, int k, const __bf16* E, float* out,
+                      hipStream_t s, int grid) {
+  switch ((k + 31) / 32) {
+    case 1: hipLaunchKernelGGL((ild_embedding_regs<R, D, 1, KIND>), grid, 256, 0, s, recs, n_users, k, E, out); break;
+    case 2: hipLaunchKernelGGL((ild_embedding_regs<R, D, 2, KIND>), grid, 256, 0, s, recs, n_users, k, E, out); break;
+    case 3: hipLaunchKernelGGL((ild_embedding_regs<R, D, 3, KIND>), grid, 256, 0, s, recs, n_users, k, E, out); break;
+    default: hipLaunchKernelGGL((ild_embedding_regs<R, D, 4, KIND>), grid, 256, 0, s, recs, n_users, k, E, out); break;
+  }
+}
+
 template <typename R, int D>
 void launch_regs(const R* recs, int64_t n_users, int k, const __bf16* E, int kind, float* out,
                  hipStream_t s, int grid) {
-  switch ((k + 31) / 32) {
-    case 1: hipLaunchKernelGGL((ild_embedding_regs<R, D, 1>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
-    case 2: hipLaunchKernelGGL((ild_embedding_regs<R, D, 2>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
-    case 3: hipLaunchKernelGGL((ild_embedding_regs<R, D, 3>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
-    default: hipLaunchKernelGGL((ild_embedding_regs<R, D, 4>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
-  }
+  if (kind == DR_ILD_COSINE) launch_regs_kind<R, D, DR_ILD_COSINE>(recs, n_users, k, E, out, s, grid);
+  else if (kind == DR_ILD_DOT) launch_regs_kind<R, D, DR_ILD_DOT>(recs, n_users, k, E, out, s, grid);
+  else launch_regs_kind<R, D, DR_ILD_EUCLIDEAN>(recs, n_users, k, E, out, s, grid);
 }
 
 template <typename R>

@@ -219,9 +219,10 @@ def test_ild_embedding(d, k, kind):
 
 
 # --------------------------------------------------------------------------- BPR + Adam
-def test_bpr_fwd_bwd():
+@pytest.mark.parametrize("d", [100, 128, 256])  # 100: the reference experiments' embedding_dim
+def test_bpr_fwd_bwd(d):
     rng = np.random.default_rng(6)
-    d, nu, ni, B = 128, 200, 300, 4096
+    nu, ni, B = 200, 300, 4096
     U = rng.standard_normal((nu, d)).astype(np.float32) * 0.3
     I = rng.standard_normal((ni, d)).astype(np.float32) * 0.3
     uid, pid, nid = rng.integers(0, nu, B), rng.integers(0, ni, B), rng.integers(0, ni, B)

@@ -1,0 +1,12 @@
+#!/bin/bash
+set -e
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/s5_gpu_tests.log 2>&1
+LIBS=product,enqloop,nut2,base
+timeout -k 10 300 python -u tools/variant_bench.py --libs $LIBS --users 131072 --items 10000000 --dim 128 --rounds 3 > gpurun_out/s5_bench128.json 2> gpurun_out/s5_bench128.err
+timeout -k 10 300 python -u tools/variant_bench.py --libs $LIBS --users 262144 --items 1000000 --dim 64 --rounds 3 > gpurun_out/s5_bench64.json 2> gpurun_out/s5_bench64.err
+bash tools/gpu_diag.sh
+for w in score1m gather bpr mmr; do
+  timeout -k 10 300 python -u bench.py --workload $w > gpurun_out/s5_wl_$w.json 2> gpurun_out/s5_wl_$w.err
+done
