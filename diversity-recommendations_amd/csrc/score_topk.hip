@@ -12,7 +12,7 @@
 //   * Each wave keeps the bf16 embeddings of its NU_T*32 users resident in
 //     registers as MFMA B fragments for the whole scan.
 //   * Item rows go HBM -> LDS by LDS-DMA (global_load_lds_dwordx4) into a ring
-//     of 32-KB stages filled kRing-1 = 3 stages ahead; the LDS image is
+//     of 32-KB stages filled kRing-1 = 2 stages ahead; the LDS image is
 //     XOR-swizzled through the per-lane source address so the A-fragment
 //     ds_read_b128s are bank-conflict-free. All 8 waves share every stage.
 //     A fragments are read two k-steps ahead of the MFMAs that use them.
@@ -72,7 +72,7 @@ enum {
 #define DR_STAGE_BYTES 32768  // one LDS ring slot
 #endif
 #ifndef DR_RING
-#define DR_RING 4  // ring slots (kRing - 1 stages in flight)
+#define DR_RING 3  // ring slots (kRing - 1 stages in flight)
 #endif
 #ifndef DR_NUT
 #define DR_NUT 4  // user tiles of 32 per wave for d <= 128
@@ -85,6 +85,16 @@ enum {
 #endif
 #ifndef DR_FLUSH_GAP
 #define DR_FLUSH_GAP 96  // new keys a buffer takes past k + kSlack before compaction
+#endif
+#ifndef DR_ENQ_STAGED
+// survivors: 0 = direct per-lane enqueue, 1 = stage lane blocks in LDS and
+// resolve them per stage, 2 = staged for d <= 64 only (measured: staged is 4%
+// faster at d=64, where survivors per MFMA are twice as dense, and 4% slower
+// at d=128)
+#define DR_ENQ_STAGED 2
+#endif
+#ifndef DR_STAGE_BLOCKS
+#define DR_STAGE_BLOCKS 64  // staged lane blocks per wave (>= 64: one user tile always fits)
 #endif
 #ifndef DR_PREPASS
 #define DR_PREPASS 0  // seed thresholds from a sample scan (measured: 1-4% slower)
@@ -363,7 +373,14 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
   constexpr int UPWG = UPW * kWaves;  // users per workgroup
   constexpr int P = CAP / 64;         // keys per lane in a compaction
   constexpr int RING_BYTES = kRing * kStageBytes;
-  constexpr int WAVE_BYTES = UPW * 4 + 256 * 4;  // per-user key counts + radix histogram
+  // per wave: per-user key counts, radix histogram, staged survivor blocks
+  // (16 scores + item base + slot + threshold each)
+  constexpr bool STAGED = DR_ENQ_STAGED == 1 || (DR_ENQ_STAGED == 2 && D <= 64);
+  constexpr int SB = STAGED ? DR_STAGE_BLOCKS : 0;
+  // stage_hits resolves a full stage area, then stages up to 64 lanes of one
+  // user tile: the area must hold a whole wave's worth of blocks
+  static_assert(!STAGED || SB >= 64, "staging area smaller than a wave");
+  constexpr int WAVE_BYTES = UPW * 4 + 256 * 4 + SB * (64 + 12);
   static_assert(RING_BYTES + kWaves * WAVE_BYTES <= 163840, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[RING_BYTES + kWaves * WAVE_BYTES];
 
@@ -388,6 +405,10 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
   char* wbase = smem + RING_BYTES + wave * WAVE_BYTES;
   uint32_t* ucnt = reinterpret_cast<uint32_t*>(wbase);
   uint32_t* hist = reinterpret_cast<uint32_t*>(wbase + UPW * 4);
+  float* blk_val = reinterpret_cast<float*>(wbase + UPW * 4 + 1024);  // [SB][16], 16-B aligned
+  uint32_t* blk_gbase = reinterpret_cast<uint32_t*>(blk_val + SB * 16);
+  uint32_t* blk_slot = blk_gbase + SB;  // slot | h << 16 | valid rows << 17
+  float* blk_thr = reinterpret_cast<float*>(blk_slot + SB);
   const uint32_t lds_ring = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
   // This lane's A-fragment byte offset for k-step s in a tile is
   // col*2D + ((2s + h) ^ swz(col)) * 16 = a_row + ((2s) ^ a_sw) * 16: two VALU
@@ -565,7 +586,8 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
           const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
           if (has) {
             const uint32_t pos = atomicAdd(&ucnt[ut * 32 + col], 1u);
-            st64(ubuf + pos, dr::make_key(v, gbase + (uint32_t)row));
+            if (pos < (uint32_t)CAP)  // always true (flush_at + MARGIN <= CAP): a guard only
+              st64(ubuf + pos, dr::make_key(v, gbase + (uint32_t)row));
           }
           vmc += 1;  // the store above issued once (some lane had a key)
         }
@@ -601,14 +623,106 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       for (int i = 0; i < kRing - 1; ++i)
         if (i == st) vs[i] = vmc;
     }
+    // Staged survivors. In the tile loop a lane whose 16 scores of a user tile
+    // beat the user's threshold only copies them to an LDS block (four
+    // ds_write_b128 + its item base, slot and threshold); resolve() later
+    // turns the staged blocks into candidate keys with one lane per block, so
+    // the per-score tests, value selects and LDS counter atomics run in
+    // parallel across blocks, off the MFMA loop. A block's threshold is the one
+    // at staging time: thresholds only rise, so it admits a superset.
+    int nblk = 0;  // staged blocks (wave-uniform)
+    auto resolve = [&]() {
+      DG_T0(t_d);
+      wave_lds_sync();
+#pragma unroll 1
+      for (int b0 = 0; b0 < nblk; b0 += 64) {
+        const int i = b0 + lane;
+        const bool live = i < nblk;
+        const int ii = live ? i : 0;
+        const uint32_t gb = blk_gbase[ii];
+        const uint32_t info = blk_slot[ii];  // slot | h << 16 | valid rows << 17
+        const float th = blk_thr[ii];
+        const uint32_t slot = info & 0xffffu;
+        const int hh = (int)((info >> 16) & 1u);
+        const int vld = live ? (int)(info >> 17) : 0;
+        uint64_t* ubuf = cbase + (size_t)slot * CAP;
+        const float4* src = reinterpret_cast<const float4*>(blk_val + ii * 16);
+        // four registers (one float4) at a time: few VGPRs, so this also runs
+        // inside stage_hits with the accumulators live
+#pragma unroll 1
+        for (int q = 0; q < 4; ++q) {
+          const float4 v4 = src[q];
+          const float vq[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = j + 8 * q + 4 * hh;  // score register r = 4q + j
+            const bool hit = row < vld && vq[j] > th;
+            if (__ballot(hit) != 0ull) {
+              if (hit) {
+                const uint32_t pos = atomicAdd(&ucnt[slot], 1u);
+                // pos < CAP always holds (flush_at + MARGIN <= CAP); the test
+                // keeps a broken invariant from ever writing past the buffer
+                if (pos < (uint32_t)CAP) st64(ubuf + pos, dr::make_key(vq[j], gb + (uint32_t)row));
+              }
+              vmc += 1;  // one store instruction (some lane had a key)
+            }
+          }
+        }
+      }
+      nblk = 0;
+      wave_lds_sync();
+      DG_ADD(kDgDrain, t_d);
+      DG_CNT(kDgNDrain);
+    };
+    auto stage_hits = [&](int t, f32x16 (&acc)[NU_T], uint32_t hit_bits) {
+      DG_T0(t_e);
+      const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
+      const int valid = (int)((i_end - tile0) < kTileItems ? (i_end - tile0) : kTileItems);
+      const uint32_t gbase = (uint32_t)(a.item_base + tile0);
+#pragma unroll
+      for (int ut = 0; ut < NU_T; ++ut) {
+        if (!(hit_bits & (1u << ut))) continue;
+        float m = acc[ut][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) m = fmaxf(m, acc[ut][r]);
+        const bool hit = m > thr[ut];
+        const uint64_t bal = __ballot(hit);
+        if (bal == 0ull) continue;
+        const int n = __popcll(bal);
+        if (nblk + n > SB) resolve();  // rare (a scan's first stages): few registers
+        if (hit) {
+          const int i = nblk + lane_prefix(bal);
+          float4* dst = reinterpret_cast<float4*>(blk_val + i * 16);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            dst[q] = make_float4(acc[ut][4 * q], acc[ut][4 * q + 1], acc[ut][4 * q + 2],
+                                 acc[ut][4 * q + 3]);
+          blk_gbase[i] = gbase;
+          blk_slot[i] = (uint32_t)(ut * 32 + col) | ((uint32_t)h << 16) | ((uint32_t)valid << 17);
+          blk_thr[i] = thr[ut];
+        }
+        nblk += n;
+      }
+      DG_ADD(kDgEnqueue, t_e);
+      DG_CNT(kDgNEnqueue);
+    };
     auto epilogue = [&](int t, f32x16 (&acc)[NU_T]) {
       DG_T0(t_h);
       uint32_t hit_bits = any_hits(acc);
       DG_ADD(kDgHits, t_h);
       hit_bits = __builtin_amdgcn_readfirstlane(hit_bits);  // ballots: uniform
-      if (hit_bits != 0u) enqueue(t, acc, hit_bits);
-      // end of a stage: compact the buffers that passed flush_at
-      if ((t + 1) % SR == 0 || t + 1 == ntiles) check_compact();
+      if constexpr (STAGED) {
+        if (hit_bits != 0u) stage_hits(t, acc, hit_bits);
+        // end of a stage: resolve the staged blocks, compact full buffers
+        if ((t + 1) % SR == 0 || t + 1 == ntiles) {
+          if (nblk > 0) resolve();
+          check_compact();
+        }
+      } else {
+        if (hit_bits != 0u) enqueue(t, acc, hit_bits);
+        // end of a stage: compact the buffers that passed flush_at
+        if ((t + 1) % SR == 0 || t + 1 == ntiles) check_compact();
+      }
     };
     // One accumulator set: the partner wave on the same SIMD issues its MFMAs
     // while this wave runs the epilogue (two waves per SIMD by design).

@@ -9,3 +9,5 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1
+cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python bench.py --workload score1m > gpurun_out/wl_score1m.json 2> gpurun_out/wl_score1m.err
