@@ -12,7 +12,8 @@
 //   * Each wave keeps the bf16 embeddings of its NU_T*32 users resident in
 //     registers as MFMA B fragments for the whole scan.
 //   * Item rows go HBM -> LDS by LDS-DMA (global_load_lds_dwordx4) into a ring
-//     of 32-KB stages filled kRing-1 = 2 stages ahead; the LDS image is
+//     of stages (d = 128: two 64-KB slots, one stage ahead; else three
+//     32-KB slots, two ahead), one s_barrier per stage; the LDS image is
 //     XOR-swizzled through the per-lane source address so the A-fragment
 //     ds_read_b128s are bank-conflict-free. All 8 waves share every stage.
 //     A fragments are read two k-steps ahead of the MFMAs that use them.
@@ -69,10 +70,16 @@ enum {
 // overrides exist so tools/variant_bench.py can time alternatives side by side
 // (build_native.py --variant NAME -D KEY=VAL).
 #ifndef DR_STAGE_BYTES
-#define DR_STAGE_BYTES 32768  // one LDS ring slot
+#define DR_STAGE_BYTES 32768  // one LDS ring slot, d != 128
 #endif
 #ifndef DR_RING
-#define DR_RING 3  // ring slots (kRing - 1 stages in flight)
+#define DR_RING 3  // ring slots (RING - 1 stages in flight), d != 128
+#endif
+#ifndef DR_STAGE_BYTES_WIDE
+#define DR_STAGE_BYTES_WIDE 65536  // ring slot for d = 128
+#endif
+#ifndef DR_RING_WIDE
+#define DR_RING_WIDE 2  // ring slots for d = 128
 #endif
 #ifndef DR_NUT
 #define DR_NUT 4  // user tiles of 32 per wave for d <= 128
@@ -106,20 +113,28 @@ enum {
 constexpr int kWaves = 8;  // two waves per SIMD: 256-register budget each
 constexpr int kThreads = kWaves * 64;
 constexpr int kTileItems = 32;
-constexpr int kStageBytes = DR_STAGE_BYTES;
-constexpr int kLpt = kStageBytes / 16 / kThreads;  // LDS-DMA per thread per stage
-constexpr int kRing = DR_RING;
 constexpr int kSlack = 32;   // keys kept beyond k by a compaction
 constexpr int kFlushGap = DR_FLUSH_GAP;
-static_assert(kLpt >= 1 && kStageBytes % (16 * kThreads) == 0, "stage geometry");
-static_assert(kRing >= 2, "ring depth");
+
+// Stage geometry per row width. d = 128: two 64-KB slots (one barrier per
+// 8 tiles at d=128; measured against three 32-KB slots: +2 % at 10M items,
+// +6 % at 1.25M, where the survivor stream makes per-stage wave imbalance
+// larger). d <= 64: three 32-KB slots (its LDS survivor staging needs room;
+// 64-KB stages measured -10 % there; d = 256 spills with them).
+constexpr int stage_bytes_for(int d) { return d == 128 ? DR_STAGE_BYTES_WIDE : DR_STAGE_BYTES; }
+constexpr int ring_for(int d) { return d == 128 ? DR_RING_WIDE : DR_RING; }
 
 template <int D>
 struct TileGeom {
+  static constexpr int STAGE_BYTES = stage_bytes_for(D);  // one LDS ring slot
+  static constexpr int RING = ring_for(D);                // slots (RING - 1 stages in flight)
+  static constexpr int LPT = STAGE_BYTES / 16 / kThreads;  // LDS-DMA per thread per stage
   static constexpr int KSTEPS = D / 16;                 // MFMA k-steps per row
   static constexpr int CPR = D / 8;                     // 16-B chunks per row
   static constexpr int TILE_BYTES = kTileItems * D * 2;
-  static constexpr int SR = kStageBytes / TILE_BYTES;   // row tiles per stage
+  static constexpr int SR = STAGE_BYTES / TILE_BYTES;   // row tiles per stage
+  static_assert(LPT >= 1 && STAGE_BYTES % (16 * kThreads) == 0, "stage geometry");
+  static_assert(RING >= 2, "ring depth");
   static constexpr int RPB = (2 * D >= 256) ? 1 : 256 / (2 * D);  // rows per 256-B bank row
   static constexpr int SWM = (CPR < 16 ? CPR : 16) - 1;
   static constexpr int MARGIN = SR * kTileItems;  // max new keys per user per stage
@@ -202,7 +217,7 @@ __device__ __forceinline__ void issue_stage(const __bf16* __restrict__ I, int64_
   const int64_t left = n_items - 1 - row0;
   const int rmax = left < ROWS - 1 ? (int)left : ROWS - 1;
 #pragma unroll
-  for (int j = 0; j < kLpt; ++j) {
+  for (int j = 0; j < G::LPT; ++j) {
     const int wave_first = j * kThreads + wave * 64;  // wave-uniform chunk index
     const int idx = wave_first + lane;
     const int r = idx / G::CPR;
@@ -372,6 +387,9 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
   constexpr int UPW = NU_T * 32;      // users per wave
   constexpr int UPWG = UPW * kWaves;  // users per workgroup
   constexpr int P = CAP / 64;         // keys per lane in a compaction
+  constexpr int kRing = G::RING;
+  constexpr int kStageBytes = G::STAGE_BYTES;
+  constexpr int kLpt = G::LPT;
   constexpr int RING_BYTES = kRing * kStageBytes;
   // per wave: per-user key counts, radix histogram, staged survivor blocks
   // (16 scores + item base + slot + threshold each)
@@ -917,7 +935,9 @@ int device_cus() {
   return cus > 0 ? cus : 256;
 }
 
-int64_t stage_items_for(int d) { return (int64_t)(kStageBytes / (kTileItems * d * 2)) * kTileItems; }
+int64_t stage_items_for(int d) {
+  return (int64_t)(stage_bytes_for(d) / (kTileItems * d * 2)) * kTileItems;
+}
 
 // Smallest candidate capacity that leaves at least 32 keys of headroom above
 // k + kSlack once a stage's worth of new keys (the margin) is reserved.
