@@ -5,12 +5,16 @@ d=128, top-100 (BASELINE.json metric; configs[3], the 10M-item catalog).
     torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 One step = one pass of the hot path over the whole synthetic workload:
-  score_topk (bf16 MFMA scores of every user x every item of this rank's item
-  shard, fused top-k) -> [N>1: all_to_all of the partial top-k lists over RCCL
-  + merge] -> cosine ILD of the final top-k lists (users sharded over ranks).
-Inputs are resident in HBM before timing. Item rows are sharded contiguously
-over ranks (the item table is also replicated for the ILD gathers); the total
-work is fixed, so scaling is "strong". value = U*I / step time (max over ranks).
+  score_topk (bf16 MFMA scores of every user of this rank's user slice x every
+  item of its item shard, fused top-k) -> [item shards > 1: all_to_all of the
+  partial top-k lists inside the rank's grid row over RCCL + merge] -> cosine
+  ILD of the final top-k lists of this rank's users.
+Ranks form a (N/S) x S grid (divrec.distributed.grid_layout): the S ranks of
+a row row-shard the item table contiguously and share one user slice. S =
+--item-shards (auto: 2 for even N; `--item-shards N` is pure item sharding).
+Inputs are resident in HBM before timing (the item table is also replicated
+for the ILD gathers); the total work is fixed, so scaling is "strong".
+value = U*I / step time (max over ranks).
 
 Rank 0 prints ONE JSON line. The `roofline` object is for the dominant kernel
 (score_topk: bound = MFMA, achieved = 2*U*I_shard*d flop / average HIP-event
@@ -41,7 +45,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from divrec import ops  # noqa: E402
-from divrec.distributed import exchange_partials, shard_range  # noqa: E402
+from divrec.distributed import exchange_partials, grid_layout, shard_range  # noqa: E402
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
@@ -59,6 +63,9 @@ def parse():
     ap.add_argument("--ild-kind", default="cosine")
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--item-shards", type=int, default=0,
+                    help="ranks that row-shard the item table per user slice (0 = auto: "
+                         "2 for an even world size, else the world size)")
     ap.add_argument("--workload", default="catalog",
                     choices=["catalog", "score1m", "gather", "bpr", "mmr"])
     return ap.parse_args()
@@ -138,15 +145,20 @@ def main():
         print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    S = 1
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        S = args.item_shards or (2 if world % 2 == 0 else world)
+    lay = grid_layout(S) if world > 1 else None
 
     U_n, I_n, d, k = args.users, args.items, args.dim, args.k
-    users = gen_table(U_n, d, 1, dev)
-    items = gen_table(I_n, d, 2, dev)  # replicated: ILD gathers arbitrary rows
-    lo, hi = shard_range(I_n, world, rank)
+    # (user slice) x (item shard) of this rank in the grid; the item table is
+    # also replicated in full for the ILD gathers
+    u_lo, u_hi = lay.user_range(U_n) if lay else (0, U_n)
+    lo, hi = lay.item_range(I_n) if lay else (0, I_n)
+    users = gen_table(U_n, d, 1, dev)[u_lo:u_hi].contiguous()
+    items = gen_table(I_n, d, 2, dev)
     shard = items[lo:hi]
-    u_lo, u_hi = shard_range(U_n, world, rank)
     torch.cuda.synchronize()
 
     ev = {n: [] for n in ("topk0", "topk1", "ild0", "ild1")}
@@ -158,8 +170,8 @@ def main():
         s, i = ops.score_topk(users, shard, k, item_base=lo)
         if e:
             e[1].record()
-        if world > 1:
-            ps, pi = exchange_partials(s, i)
+        if S > 1:  # partial lists of this rank's sub-slice from its row, merged
+            ps, pi = exchange_partials(s, i, lay.group)
             s, i = ops.topk_merge(ps, pi, k)
         if e:
             e[2].record()
@@ -191,7 +203,7 @@ def main():
     step_s = dt / args.steps
 
     cfg_key = f"U{U_n}_I{I_n}_d{d}_k{k}_G{world}"
-    flops = 2.0 * U_n * (hi - lo) * d
+    flops = 2.0 * (u_hi - u_lo) * (hi - lo) * d
     achieved = flops / topk_s / 1e12
     traffic = load_traffic(cfg_key)
     result = {
@@ -209,9 +221,12 @@ def main():
         "data": "synthetic (N(0,1/sqrt(d)) bf16 tables, seeded per 1M-row block)",
         "config": {
             "workload": f"score_topk + cosine ILD: {U_n} users x {I_n} items, d={d}, k={k} "
-                        f"(BASELINE configs[3], item rows sharded over ranks)",
+                        f"(BASELINE configs[3]; ranks in a {world // S} x {S} grid: item rows "
+                        f"sharded {S} ways, users {world // S} ways)",
             "users": U_n, "items": I_n, "dim": d, "k": k,
-            "parallelism": f"item-shard{world}" + ("+all_to_all" if world > 1 else ""),
+            "parallelism": f"item-shard{S}" + (f"+all_to_all(group of {S})" if S > 1 else "")
+                           + (f" x user-shard{world // S}" if world // S > 1 else ""),
+            "item_shards": S,
         },
         "ild_users_per_s": U_n / ild_max,
         "score_topk_ms": topk_s * 1e3,

@@ -16,15 +16,24 @@ xGMI on ROCm):
 Because the order (score desc, item id asc) is a total order and a score does
 not depend on which shard computed it, the merged lists are bit-identical to
 single-device dr_score_topk over the whole catalog.
+
+Grid layout (``grid_layout``): the G ranks form a (G / S) x S grid. The S
+ranks of a row share one user slice and row-shard the item table S ways; the
+exchange above runs inside the row (a process group of S ranks). S = G is
+pure item sharding; S = 1 is pure user sharding (no exchange). The scan's
+survivor stream costs ~users * k * ln(items / k) per rank, so at fixed U x I
+fewer item shards mean less of it.
 """
 from __future__ import annotations
 
-from typing import Callable, Optional, Tuple
+from dataclasses import dataclass
+from typing import Any, Callable, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
 Partial = Tuple[torch.Tensor, torch.Tensor]  # (scores fp32 [n, k], items int32 [n, k])
+_SOLO = "solo"  # group sentinel: this rank alone holds the whole catalog (no exchange)
 
 
 def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
@@ -32,6 +41,44 @@ def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
     base, rem = divmod(n, world)
     lo = rank * base + min(rank, rem)
     return lo, lo + base + (1 if rank < rem else 0)
+
+
+@dataclass
+class GridLayout:
+    """This rank's place in a (user_groups x item_shards) grid of ranks."""
+
+    world: int
+    rank: int
+    item_shards: int   # S: ranks that row-shard the item table for one user slice
+    user_groups: int   # G / S
+    item_shard: int    # column of this rank: item rows shard_range(I, S, item_shard)
+    user_group: int    # row of this rank: users shard_range(U, G / S, user_group)
+    group: Any         # process group of this row (None = the default group)
+
+    def item_range(self, n_items: int) -> Tuple[int, int]:
+        return shard_range(n_items, self.item_shards, self.item_shard)
+
+    def user_range(self, n_users: int) -> Tuple[int, int]:
+        return shard_range(n_users, self.user_groups, self.user_group)
+
+
+def grid_layout(item_shards: int) -> GridLayout:
+    """Place every rank of the default group in the grid; ranks u*S .. u*S+S-1
+    form row u. Collective: every rank must call it (dist.new_group)."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if item_shards < 1 or world % item_shards:
+        raise ValueError(f"item_shards={item_shards} must divide the world size {world}")
+    groups = world // item_shards
+    group = None
+    if 1 < item_shards < world:
+        for u in range(groups):  # every rank creates every row group, in the same order
+            g = dist.new_group(list(range(u * item_shards, (u + 1) * item_shards)))
+            if u == rank // item_shards:
+                group = g
+    if item_shards == 1:
+        group = _SOLO
+    return GridLayout(world, rank, item_shards, groups, rank % item_shards,
+                      rank // item_shards, group)
 
 
 def exchange_partials(scores: torch.Tensor, items: torch.Tensor, group=None) -> Partial:
@@ -76,8 +123,8 @@ def sharded_score_topk(
 
         local_topk = local_topk or ops.score_topk
         merge = merge or ops.topk_merge
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    world = 1 if group is _SOLO else dist.get_world_size(group)
+    rank = 0 if group is _SOLO else dist.get_rank(group)
     n = user_table.size(0) if user_ids is None else user_ids.numel()
     s, i = local_topk(user_table, item_shard, k, user_ids=user_ids, item_base=item_base)
     if world == 1:

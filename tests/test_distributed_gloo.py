@@ -104,3 +104,49 @@ def test_exchange_routes_user_slices():
         for src in range(world):   # row block `src` came from rank src, users lo..hi
             assert np.array_equal(i[src, :, 0], src * 1000 + np.arange(lo, hi))
             assert np.allclose(s[src, :, 0], src + np.arange(lo, hi) / 10)
+
+
+def _grid_worker(rank, world, port, S, U, I, k, q):
+    from divrec.distributed import grid_layout
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lay = grid_layout(S)
+        ulo, uhi = lay.user_range(U.shape[0])
+        lo, hi = lay.item_range(I.shape[0])
+        (s, i), (a, b) = sharded_score_topk(torch.from_numpy(U[ulo:uhi]), torch.from_numpy(I[lo:hi]),
+                                            lo, k, group=lay.group, local_topk=_local_topk,
+                                            merge=_merge)
+        q.put((rank, lay.user_group, lay.item_shard, ulo + a, ulo + b, s.numpy(), i.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,S", [(4, 2), (4, 1), (4, 4), (2, 1)])
+def test_grid_layout_equals_single_device(world, S):
+    """(world/S) x S grid: users split over rows, item rows over the S ranks of a
+    row, exchange inside the row only. Every user is owned by exactly one rank
+    and its list equals the single-device top-k over the whole catalog."""
+    rng = np.random.default_rng(world * 10 + S)
+    U = rng.integers(-3, 4, size=(45, 16)).astype(np.float32)
+    I = rng.integers(-3, 4, size=(803, 16)).astype(np.float32)
+    k = 20
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, return_scores=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grid_worker, args=(r, world, port, S, U, I, k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    owned = np.zeros(U.shape[0], dtype=int)
+    for rank, ug, ish, a, b, s, i in got:
+        assert (ug, ish) == (rank // S, rank % S)
+        assert np.array_equal(i, ref_i[a:b])
+        assert np.array_equal(s, ref_s[a:b].astype(np.float32))
+        owned[a:b] += 1
+    assert (owned == 1).all()
