@@ -269,3 +269,68 @@ def test_mmr_rerank(lam):
     if lam == 1.0:  # pure relevance: equals top-k by score (ties: lowest position)
         ref = np.take_along_axis(cand, np.argsort(-sc, axis=1, kind="stable")[:, :kout], axis=1)
         assert np.array_equal(got, ref)
+
+
+def _mmr_check_positions(picks, cand, sc, E, lam, tol):
+    """float64 replay that also handles invalid (-1) candidates: each pick must
+    be a live candidate whose MMR value is within tol of the step maximum, and
+    -1 must appear exactly when no live candidate is left."""
+    bad = 0
+    for u in range(cand.shape[0]):
+        valid = cand[u] >= 0
+        X = E[np.where(valid, cand[u], 0)].astype(np.float64)
+        Xn = X / np.linalg.norm(X, axis=1, keepdims=True)
+        sims = Xn @ Xn.T
+        s = sc[u].astype(np.float64)
+        alive = valid.copy()
+        pen = None
+        for it in picks[u]:
+            if not alive.any():
+                bad += int(it != -1)
+                continue
+            val = lam * s - (1 - lam) * (pen if pen is not None else 0.0)
+            val[~alive] = -np.inf
+            hits = np.nonzero(alive & (cand[u] == it))[0]
+            if len(hits) == 0 or val[hits].max() < val.max() - tol:
+                bad += 1
+                continue
+            j = hits[np.argmax(val[hits])]
+            alive[j] = False
+            pen = sims[:, j] if pen is None else np.maximum(pen, sims[:, j])
+    return bad
+
+
+@pytest.mark.parametrize("d,C,kout,lam", [(128, 1000, 100, 0.5), (128, 1024, 100, 0.9),
+                                          (64, 1024, 64, 0.3), (64, 777, 100, 0.0),
+                                          (128, 1000, 100, 1.0)])
+def test_mmr_rerank_config5_shape(d, C, kout, lam):
+    """Config-5 shapes (1000 -> 100, scores sorted descending as a top-k list
+    gives them); every pick a valid greedy step within 1e-4 (float64 replay)."""
+    rng = np.random.default_rng(d + C + kout)
+    ni, n = 20000, 12
+    E = oracle.as_bf16_f32((rng.standard_normal((ni, d)) / np.sqrt(d)).astype(np.float32))
+    cand = np.stack([rng.choice(ni, C, replace=False) for _ in range(n)]).astype(np.int32)
+    sc = -np.sort(-rng.random((n, C)), axis=1).astype(np.float32)
+    got = ops.mmr_rerank(torch.from_numpy(cand).to(DEV), torch.from_numpy(sc).to(DEV), _bf16(E),
+                         kout, lam).cpu().numpy()
+    assert _mmr_check_positions(got, cand, sc, E, lam, tol=1e-4) == 0
+    if lam == 1.0:
+        assert np.array_equal(got, cand[:, :kout])
+
+
+def test_mmr_rerank_invalid_candidates():
+    """-1 candidates are never picked; once the live ones run out the tail is -1."""
+    rng = np.random.default_rng(5)
+    d, ni, n, C, kout = 64, 3000, 6, 200, 150
+    E = oracle.as_bf16_f32(rng.standard_normal((ni, d)).astype(np.float32))
+    cand = np.stack([rng.choice(ni, C, replace=False) for _ in range(n)]).astype(np.int32)
+    for u in range(n):  # 0, 35, 70, ... invalid entries: fewer live than kout for most users
+        cand[u, rng.choice(C, 35 * u, replace=False)] = -1
+    sc = rng.standard_normal((n, C)).astype(np.float32)
+    got = ops.mmr_rerank(torch.from_numpy(cand).to(DEV), torch.from_numpy(sc).to(DEV), _bf16(E),
+                         kout, 0.6).cpu().numpy()
+    assert _mmr_check_positions(got, cand, sc, E, 0.6, tol=1e-4) == 0
+    for u in range(n):
+        n_live = int((cand[u] >= 0).sum())
+        assert (got[u, :min(n_live, kout)] >= 0).all()
+        assert (got[u, n_live:] == -1).all()
