@@ -133,6 +133,48 @@ def test_score_topk_chunked_catalog_exact():
     assert np.array_equal(s.cpu().numpy(), ref_s)
 
 
+def test_score_topk_guess_rescan_exact():
+    """Catalogs >= 2^18 rows start from a threshold guessed on a strided sample
+    (every 32nd row) and rescan users the guess failed. Here the sampled rows
+    0, 32, ... 288 are "hot": the best items of every non-negative user (group
+    A), so A's guess admits only those 10 items (< k) and all of A must be
+    rescanned; non-positive users (group B) rank them last and are not. With
+    duplicate / permuted user ids and exclusions (some hot items excluded)
+    the lists must equal the oracle's exactly."""
+    rng = np.random.default_rng(77)
+    d, ni, k = 64, (1 << 18) + 123, 50
+    U = np.concatenate([_int_table(rng, 48, d, 0, 3), _int_table(rng, 48, d, -3, 0)])
+    I = _int_table(rng, ni, d)
+    I[np.arange(10) * 32] = 3.0  # hot sample rows
+    users = np.concatenate([rng.permutation(96), rng.integers(0, 96, 24)]).astype(np.int64)
+    frozen = [rng.choice(ni, size=rng.integers(0, 50), replace=False) for _ in users]
+    for n in range(0, len(users), 4):
+        frozen[n] = np.union1d(frozen[n], [0, 64, 288])
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    s, it = ops.score_topk(_bf16(U), _bf16(I), k, user_ids=torch.from_numpy(users).to(DEV),
+                           exclude=(torch.from_numpy(rowptr).to(DEV), torch.from_numpy(cols).to(DEV)))
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, users=users, frozen=frozen, return_scores=True)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy(), ref_s)
+
+
+def test_score_topk_guess_float_large():
+    """Guessed-threshold path on a float catalog (2^19 rows, d=128): every user
+    takes the guess (few or no rescans), lists within the float tolerance."""
+    rng = np.random.default_rng(3)
+    d, k = 128, 100
+    U = oracle.as_bf16_f32(rng.standard_normal((64, d)).astype(np.float32) / np.sqrt(d))
+    I = oracle.as_bf16_f32(rng.standard_normal((1 << 19, d)).astype(np.float32) / np.sqrt(d))
+    s, it = ops.score_topk(_bf16(U), _bf16(I), k)
+    s, it = s.cpu().numpy(), it.cpu().numpy().astype(np.int64)
+    S = U.astype(np.float64) @ I.astype(np.float64).T
+    tol = 1e-5 * np.sqrt(d / 64)
+    kth = -np.sort(-S, axis=1)[:, k - 1]
+    assert np.all(np.abs(s - np.take_along_axis(S, it, axis=1)) <= tol)
+    for u in range(S.shape[0]):
+        assert np.isin(np.nonzero(S[u] > kth[u] + 2 * tol)[0], it[u]).all()
+
+
 def test_score_topk_float_tolerance():
     rng = np.random.default_rng(2)
     d, k = 128, 100
