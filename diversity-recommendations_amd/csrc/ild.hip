@@ -190,7 +190,10 @@ __global__ __launch_bounds__(256) void ild_embedding_kernel(const R* __restrict_
 // pair mask is structural (off-diagonal tiles need only j < k). Fragments:
 // NT * D/16 * 4 VGPRs (128 at NT=4, D=128).
 template <typename R, int D, int NT, int KIND>
-__global__ __launch_bounds__(256) void ild_embedding_regs(const R* __restrict__ recs,
+// (NT < 4: ask for two waves per SIMD, which fits without spills and is 13 %
+// faster at k=10; the NT=4 list needs the full register file, measured 35 %
+// slower when squeezed; profiles/r01_ild_ab_*.json)
+__global__ __launch_bounds__(256, NT < 4 ? 2 : 1) void ild_embedding_regs(const R* __restrict__ recs,
                                                           int64_t n_users, int k,
                                                           const __bf16* __restrict__ E,
                                                           float* __restrict__ out) {
