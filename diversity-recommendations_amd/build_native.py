@@ -89,6 +89,27 @@ def build(jobs: int = 4, verbose: bool = False, diag: bool = False, variant: str
     return lib_path
 
 
+PEAKS_SRC = PKG_ROOT.parent / "tools" / "peaks.hip"
+PEAKS_LIB = PKG_ROOT.parent / "tools" / "_peaks" / "libdivrec_peaks.so"
+
+
+def build_peaks(verbose: bool = False) -> Path:
+    """tools/peaks.hip -> tools/_peaks/libdivrec_peaks.so: the achievable-peak
+    probes bench.py reports beside the vendor peaks (measurement only, not
+    part of the product library)."""
+    PEAKS_LIB.parent.mkdir(parents=True, exist_ok=True)
+    if PEAKS_LIB.exists() and PEAKS_LIB.stat().st_mtime >= PEAKS_SRC.stat().st_mtime:
+        return PEAKS_LIB
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-shared",
+           str(PEAKS_SRC), "-o", str(PEAKS_LIB)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for peaks.hip:\n{r.stdout}\n{r.stderr}")
+    return PEAKS_LIB
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
@@ -100,6 +121,8 @@ def main() -> int:
     args = ap.parse_args()
     path = build(args.jobs, args.verbose, args.diag, args.variant, args.defines)
     print(path)
+    if not args.variant and not args.diag:
+        print(build_peaks(args.verbose))
     return 0
 
 
