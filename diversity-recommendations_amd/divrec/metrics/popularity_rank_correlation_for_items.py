@@ -1,11 +1,13 @@
 """Popularity-rank correlation PRI (reference
 divrec/metrics/popularity_rank_correlation_for_items.py:6-63): Pearson
 correlation between an item's popularity rank and its average position in the
-recommendation lists. Catalog-level statistic (SURVEY.md §8f rank 2, next
-tier): tensor ops, the per-item average position by a scatter instead of the
-reference's Python dict loop."""
+recommendation lists. Catalog-level statistic: the
+per-item counts and position sums come from one HIP kernel
+(dr_catalog_histogram, exact integer atomics) instead of the reference's
+Python dict loop; the correlation is the reference's tensor expression."""
 import torch
 
+from divrec import _backend, ops
 from divrec.losses.base_losses import DatasetAwareLoss, RecommendationsAwareLoss
 
 
@@ -25,15 +27,18 @@ def spearman_rank_correlation(a: torch.Tensor, b: torch.Tensor, evaluate_rank: b
     return torch.mean((a - a_mean) * (b - b_mean)) / a_std / b_std
 
 
-def avg_rank(recommendations: torch.LongTensor):
-    """(items ascending, mean position of each item over all lists)."""
-    n, k = recommendations.shape
-    flat = recommendations.reshape(-1)
-    pos = torch.arange(k, device=recommendations.device).repeat(n).to(torch.float64)
-    items, inv = torch.unique(flat, return_inverse=True)
-    total = torch.zeros(items.numel(), dtype=torch.float64, device=flat.device).index_add_(0, inv, pos)
-    cnt = torch.bincount(inv, minlength=items.numel()).to(torch.float64)
-    return items, (total / cnt).to(torch.float32)
+def avg_rank(recommendations: torch.LongTensor, n_items=None):
+    """(items ascending, mean 0-based position of each item over all lists):
+    the reference's sum(r) / len(r) per item (exact integer sums, divided in
+    float64, stored as float32 like its FloatTensor)."""
+    dev = recommendations.device if recommendations.is_cuda else _backend.default_device()
+    recs = recommendations.to(dev)
+    if n_items is None:
+        n_items = int(recs.max()) + 1 if recs.numel() else 1
+    counts, pos_sum = ops.catalog_histogram(recs, int(n_items))
+    items = torch.nonzero(counts > 0).flatten()
+    avg = (pos_sum[items].to(torch.float64) / counts[items].to(torch.float64)).to(torch.float32)
+    return items, avg
 
 
 class PRI(RecommendationsAwareLoss, DatasetAwareLoss):
@@ -49,6 +54,6 @@ class PRI(RecommendationsAwareLoss, DatasetAwareLoss):
         return self.recommendations_loss(interactions, recommendations)
 
     def recommendations_loss(self, interactions, recommendations) -> torch.Tensor:
-        items, ranks = avg_rank(recommendations)
+        items, ranks = avg_rank(recommendations, int(self.dataset.number_of_items))
         pr = self.popularity_rank.to(items.device)[items]
         return spearman_rank_correlation(pr, ranks, evaluate_rank=False)

@@ -281,6 +281,24 @@ def adam_dense(
     B.check(rc, "dr_adam_dense")
 
 
+# --------------------------------------------------------------------------- catalog histogram
+def catalog_histogram(recs: torch.Tensor, n_items: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(counts int32 [n_items], position sums int64 [n_items]) of the item ids
+    in ``recs`` [n, k]; entries outside [0, n_items) are skipped."""
+    dev = B.require_device(recs)
+    recs, rc_dt = _recs(recs)
+    n, k = recs.shape
+    _need(n_items >= 1, "n_items must be >= 1")
+    counts = torch.zeros(int(n_items), dtype=torch.int32, device=dev)
+    pos_sum = torch.zeros(int(n_items), dtype=torch.int64, device=dev)
+    if n == 0 or k == 0:
+        return counts, pos_sum
+    rc = B.lib().dr_catalog_histogram(recs.data_ptr(), rc_dt, n, k, int(n_items),
+                                      counts.data_ptr(), pos_sum.data_ptr(), B.stream(dev))
+    B.check(rc, "dr_catalog_histogram")
+    return counts, pos_sum
+
+
 # --------------------------------------------------------------------------- MMR
 def mmr_rerank(
     cand_items: torch.Tensor, cand_scores: torch.Tensor, item_table: torch.Tensor, k_out: int,

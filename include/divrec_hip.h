@@ -170,6 +170,18 @@ int dr_rank_metrics(const void* recs, int rec_dtype, int64_t n_users, int k,
                     float* recall, float* avg_precision, float* ndcg, dr_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Catalog histogram of recommendation lists: ADDS, for
+ * every entry of recs [n_users, k] with 0 <= item < n_items, 1 to counts[item]
+ * (int32 [n_items]) and its 0-based position to pos_sum[item] (uint64
+ * [n_items], may be NULL). The caller zeroes both. Replaces the counting of
+ * EntropyDiversityScore (divrec/metrics/entropy_diversity_score.py:19-26,
+ * torch.unique counts) and PRI's avg_rank
+ * (divrec/metrics/popularity_rank_correlation_for_items.py:28-39). Exact. */
+int dr_catalog_histogram(const void* recs, int rec_dtype, int64_t n_users, int k,
+                         int64_t n_items, int32_t* counts, uint64_t* pos_sum,
+                         dr_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * MMR diversity re-rank (config 5; no reference symbol — SURVEY.md §8a a16):
  * per user, greedily pick k_out of the C candidates maximising
  *   lambda * score_i - (1 - lambda) * max_{j in S} cos(e_i, e_j)

@@ -376,3 +376,36 @@ def test_mmr_rerank_invalid_candidates():
         n_live = int((cand[u] >= 0).sum())
         assert (got[u, :min(n_live, kout)] >= 0).all()
         assert (got[u, n_live:] == -1).all()
+
+
+# --------------------------------------------------------------------------- catalog histogram
+@pytest.mark.parametrize("dt", [torch.int32, torch.int64])
+def test_catalog_histogram_exact(dt):
+    """Counts and 0-based position sums per item (Entropy's torch.unique counts,
+    PRI's avg_rank sums), exact; -1 and out-of-range entries are skipped."""
+    rng = np.random.default_rng(8)
+    n, k, ni = 5000, 37, 3000
+    recs = rng.integers(-1, ni + 2, size=(n, k))
+    counts, pos = ops.catalog_histogram(torch.from_numpy(recs).to(DEV, dt), ni)
+    ok = (recs >= 0) & (recs < ni)
+    ref_c = np.bincount(recs[ok], minlength=ni)
+    ref_p = np.bincount(recs[ok], weights=np.broadcast_to(np.arange(k), recs.shape)[ok], minlength=ni)
+    assert np.array_equal(counts.cpu().numpy(), ref_c)
+    assert np.array_equal(pos.cpu().numpy(), ref_p.astype(np.int64))
+
+
+def test_pri_avg_rank_matches_reference_formula():
+    """avg_rank = the reference's per-item sum(positions) / len(positions) as float32."""
+    from divrec.metrics.popularity_rank_correlation_for_items import avg_rank
+
+    rng = np.random.default_rng(13)
+    recs = rng.integers(0, 500, size=(300, 20))
+    items, avg = avg_rank(torch.from_numpy(recs).to(DEV))
+    ranks = {}
+    for row in recs:
+        for p, it in enumerate(row):
+            ranks.setdefault(int(it), []).append(p)
+    ref_items = np.array(sorted(ranks))
+    ref_avg = np.array([sum(ranks[i]) / len(ranks[i]) for i in ref_items], dtype=np.float32)
+    assert np.array_equal(items.cpu().numpy(), ref_items)
+    assert np.array_equal(avg.cpu().numpy(), ref_avg)
