@@ -115,6 +115,21 @@ __device__ __forceinline__ f32x16 gram_tile(const bf16x8 (&x)[D / 16], const bf1
   return acc;
 }
 
+// Same, but the zero accumulator is threaded through an empty asm that reads
+// `after`: the tile's MFMAs cannot be hoisted above the work that produced
+// `after`, so only one tile's accumulators are live at a time (hipcc otherwise
+// hoists all ten Gram tiles of a 128-row list: 400+ registers, one wave/SIMD).
+template <int D>
+__device__ __forceinline__ f32x16 gram_tile_after(const bf16x8 (&x)[D / 16],
+                                                  const bf16x8 (&y)[D / 16], float after) {
+  f32x16 acc = f32x16{};
+  asm volatile("" : "+v"(acc) : "v"(after));
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s)
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[s], y[s], acc, 0, 0, 0);
+  return acc;
+}
+
 constexpr int kEmbMaxK = 128;
 
 template <typename R, int D>
@@ -190,10 +205,10 @@ __global__ __launch_bounds__(256) void ild_embedding_kernel(const R* __restrict_
 // pair mask is structural (off-diagonal tiles need only j < k). Fragments:
 // NT * D/16 * 4 VGPRs (128 at NT=4, D=128).
 template <typename R, int D, int NT, int KIND>
-// (NT < 4: ask for two waves per SIMD, which fits without spills and is 13 %
-// faster at k=10; the NT=4 list needs the full register file, measured 35 %
-// slower when squeezed; profiles/r01_ild_ab_*.json)
-__global__ __launch_bounds__(256, NT < 4 ? 2 : 1) void ild_embedding_regs(const R* __restrict__ recs,
+// Two waves per SIMD: with the Gram tiles serialised (gram_tile_after) even
+// the 128-row list fits in 256 registers, so one wave's row gathers overlap
+// the other's MFMAs (profiles/r01_ild_ab_*.json).
+__global__ __launch_bounds__(256, 2) void ild_embedding_regs(const R* __restrict__ recs,
                                                           int64_t n_users, int k,
                                                           const __bf16* __restrict__ E,
                                                           float* __restrict__ out) {
@@ -240,7 +255,9 @@ __global__ __launch_bounds__(256, NT < 4 ? 2 : 1) void ild_embedding_regs(const 
     }
 #pragma unroll
     for (int tj = ti; tj < NT; ++tj) {
-      const f32x16 g = gram_tile<D>(x[ti], x[tj]);
+      f32x16 g;
+      if constexpr (NT >= 3) g = gram_tile_after<D>(x[ti], x[tj], sum);  // registers are the limit
+      else g = gram_tile<D>(x[ti], x[tj]);  // short lists: let the scheduler overlap tiles
       const int j = 32 * tj + col;
       const bool jv = j < k;
       const float wj = (KIND != DR_ILD_DOT && jv) ? w[j] : 0.f;
