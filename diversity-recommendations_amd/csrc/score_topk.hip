@@ -26,7 +26,7 @@
 //     k + kSlack + kFlushGap keys the wave compacts it with an in-register
 //     radix select, keeping only keys that can still reach the top k, and
 //     raises the user's threshold to the selected bound.
-//   * Guessed thresholds (SEEDED = true, catalogs of 2^18 .. 2^22 rows): a
+//   * Guessed thresholds (SEEDED = true, catalogs of 2^18 .. 2^23 rows): a
 //     scan of a strided sample sets each user's starting threshold; users the
 //     guess failed (fewer than k keys at the end) are rescanned from -inf.
 //   * All VMEM traffic inside the scan (LDS-DMA and candidate stores) is
@@ -1019,8 +1019,9 @@ Plan make_plan(int64_t n_users, int64_t n_items, int d, int k) {
 // users are rescanned from -inf (device-side count, no host sync). Results are
 // bit-identical to the plain scan in every case; a catalog whose sampled rows
 // are unrepresentative only pays the rescan (one extra unit scan per 1024
-// failing users). Used below kGuessMaxItems rows (measured, 6-sigma margin:
-// +14 % at d=64 over 1M items, +6 % at d=128 over 1.25M, -0.8 % over 10M).
+// failing users). Used up to kGuessMaxItems rows (measured, 6-sigma margin:
+// +14 % at d=64 over 1M items, +6 % at d=128 over 1.25M, +1.7 % over 5M,
+// -0.3 to -0.8 % over 10M).
 struct Guess {
   int64_t S = 0;       // sample rows (0 = plain scan)
   int64_t stride = 0;  // sample row i is slice row i * stride
@@ -1035,7 +1036,10 @@ struct Guess {
 #endif
 constexpr int64_t kGuessStride = 32;
 constexpr int64_t kGuessMinItems = 1 << 18;
-constexpr int64_t kGuessMaxItems = 1 << 22;
+#ifndef DR_GUESS_MAX_LOG2
+#define DR_GUESS_MAX_LOG2 23  // measured: +1.7 % at 5M rows, -0.3 % at 10M
+#endif
+constexpr int64_t kGuessMaxItems = 1ll << DR_GUESS_MAX_LOG2;
 
 Guess guess_for(int64_t n_items, int k) {
   Guess g;
