@@ -7,7 +7,7 @@
 // Kernels:
 //
 // score_scan_kernel — one 512-thread workgroup (8 waves, two per SIMD) owns
-//   UPWG = 8*NU_T*32 users (1024 for d <= 128) and streams one chunk of the
+//   UPWG = 8*NU_T*32 users (2048 for d <= 64, 1024 for d = 128) and streams one chunk of the
 //   item catalog, so every item byte staged in LDS feeds UPWG flop.
 //   * Each wave keeps the bf16 embeddings of its NU_T*32 users resident in
 //     registers as MFMA B fragments for the whole scan.
@@ -79,7 +79,10 @@ enum {
 #define DR_RING_WIDE 2  // ring slots for d = 128
 #endif
 #ifndef DR_NUT
-#define DR_NUT 4  // user tiles of 32 per wave for d <= 128
+#define DR_NUT 4  // user tiles of 32 per wave for d = 128
+#endif
+#ifndef DR_NUT_NARROW
+#define DR_NUT_NARROW 8  // user tiles of 32 per wave for d <= 64 (measured: 8 is +14 % at d=64, 1M x 1M)
 #endif
 #ifndef DR_PRIO
 #define DR_PRIO 0  // static s_setprio 1 for waves 4-7 (measured: no gain)
@@ -107,7 +110,10 @@ enum {
 constexpr int kWaves = 8;  // two waves per SIMD: 256-register budget each
 constexpr int kThreads = kWaves * 64;
 constexpr int kTileItems = 32;
-constexpr int kSlack = 32;   // keys kept beyond k by a compaction
+#ifndef DR_SLACK
+#define DR_SLACK 32
+#endif
+constexpr int kSlack = DR_SLACK;  // keys kept beyond k by a compaction
 constexpr int kFlushGap = DR_FLUSH_GAP;
 
 // Stage geometry per row width. d = 128: two 64-KB slots (one barrier per
@@ -139,8 +145,15 @@ struct TileGeom {
 };
 
 // User tiles (of 32) per wave. The B fragments take NU_T*KSTEPS*4 VGPRs (128 at
-// d=128, NU_T=4) and the accumulators NU_T*16.
-constexpr int nut_for(int d) { return d >= 256 ? 2 : DR_NUT; }
+// d=128, NU_T=4; 128 at d=64, NU_T=8). The tiles are scored in groups of at
+// most four against each item tile, one accumulator set (4*16 VGPRs) reused
+// by the groups, so narrow rows can hold more users per wave.
+constexpr int nut_for(int d) { return d >= 256 ? 2 : (d <= 64 ? DR_NUT_NARROW : DR_NUT); }
+constexpr int ngroup_for(int d) { return nut_for(d) > 4 ? 4 : nut_for(d); }
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -381,6 +394,9 @@ template <int D, int CAP, bool SEEDED>
 __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
   using G = TileGeom<D>;
   constexpr int NU_T = nut_for(D);
+  constexpr int NG = ngroup_for(D);  // user tiles per accumulator group
+  constexpr int NGRP = NU_T / NG;    // groups scored against each item tile
+  static_assert(NGRP * NG == NU_T && NGRP <= 2, "user tile groups");
   constexpr int KS = G::KSTEPS;
   constexpr int SR = G::SR;
   constexpr int UPW = NU_T * 32;      // users per wave
@@ -483,10 +499,11 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
     DG_ADD(kDgPrologue, t_pro);
 
     // -------------------------------------------------------------- MFMA tile
-    auto mma_tile = [&](int t, f32x16 (&acc)[NU_T]) {
+    auto mma_tile = [&](int t, f32x16 (&acc)[NG], auto GI) {
+      constexpr int g0 = decltype(GI)::value * NG;
       const uint32_t tb = lds_ring + ((t / SR) % kRing) * kStageBytes + (t % SR) * G::TILE_BYTES;
 #pragma unroll
-      for (int ut = 0; ut < NU_T; ++ut) acc[ut] = f32x16{};
+      for (int ut = 0; ut < NG; ++ut) acc[ut] = f32x16{};
 #if DR_APIPE
       // Fragment s is read two k-steps before its MFMAs; each wait retires
       // exactly the fragment the next MFMAs consume.
@@ -499,9 +516,9 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         else lds_wait0(af[s]);
         if (s + 2 < KS) af[s + 2] = ds_read_b128_asm(tb + a_off(s + 2));
 #pragma unroll
-        for (int ut = 0; ut < NU_T; ++ut)
+        for (int ut = 0; ut < NG; ++ut)
           acc[ut] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[s]),
-                                                            bfr[ut][s], acc[ut], 0, 0, 0);
+                                                            bfr[g0 + ut][s], acc[ut], 0, 0, 0);
       }
 #else
       constexpr int HALF = KS >= 4 ? KS / 2 : KS;
@@ -515,9 +532,9 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
 #pragma unroll
         for (int s = 0; s < HALF; ++s)
 #pragma unroll
-          for (int ut = 0; ut < NU_T; ++ut)
+          for (int ut = 0; ut < NG; ++ut)
             acc[ut] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                __builtin_bit_cast(bf16x8, af[s]), bfr[ut][s0 + s], acc[ut], 0, 0, 0);
+                __builtin_bit_cast(bf16x8, af[s]), bfr[g0 + ut][s0 + s], acc[ut], 0, 0, 0);
       }
 #endif
     };
@@ -561,14 +578,15 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
 
     // -------------------------------------------------------------- epilogues
     // Hot test (branch-free): per user tile, a 16-way max against the threshold.
-    auto any_hits = [&](f32x16 (&acc)[NU_T]) -> uint32_t {
+    auto any_hits = [&](f32x16 (&acc)[NG], auto GI) -> uint32_t {
+      constexpr int g0 = decltype(GI)::value * NG;
       uint32_t bits = 0;
 #pragma unroll
-      for (int ut = 0; ut < NU_T; ++ut) {
+      for (int ut = 0; ut < NG; ++ut) {
         float m = acc[ut][0];
 #pragma unroll
         for (int r = 1; r < 16; ++r) m = fmaxf(m, acc[ut][r]);
-        bits |= (__ballot(m > thr[ut]) != 0ull ? 1u : 0u) << ut;
+        bits |= (__ballot(m > thr[g0 + ut]) != 0ull ? 1u : 0u) << ut;
       }
       return bits;
     };
@@ -578,7 +596,8 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
     // call and no queue in the hot loop, so nothing forces the accumulators
     // and B fragments out of registers. A stage adds at most MARGIN keys per
     // user, so a buffer compacted at the stage end never overflows.
-    auto enqueue = [&](int t, f32x16 (&acc)[NU_T], uint32_t hit_bits) {
+    auto enqueue = [&](int t, f32x16 (&acc)[NG], uint32_t hit_bits, auto GI) {
+      constexpr int g0 = decltype(GI)::value * NG;
       DG_T0(t_e);
       const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
       const int valid = (int)((i_end - tile0) < kTileItems ? (i_end - tile0) : kTileItems);
@@ -593,13 +612,14 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         }
       }
 #pragma unroll
-      for (int ut = 0; ut < NU_T; ++ut) {
+      for (int ut = 0; ut < NG; ++ut) {
         if (!(hit_bits & (1u << ut))) continue;
         uint32_t mask = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mask |= (acc[ut][r] > thr[ut] ? 1u : 0u) << r;
+        for (int r = 0; r < 16; ++r) mask |= (acc[ut][r] > thr[g0 + ut] ? 1u : 0u) << r;
         mask &= vmask;
-        uint64_t* ubuf = cbase + (size_t)(ut * 32 + col) * CAP;  // this lane's user buffer
+        const int slot = (g0 + ut) * 32 + col;
+        uint64_t* ubuf = cbase + (size_t)slot * CAP;  // this lane's user buffer
         while (__ballot(mask != 0u) != 0ull) {
           const bool has = mask != 0u;
           const int r = has ? __builtin_ctz(mask) : 0;
@@ -609,7 +629,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
           for (int q = 1; q < 16; ++q) v = (r == q) ? acc[ut][q] : v;
           const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
           if (has) {
-            const uint32_t pos = atomicAdd(&ucnt[ut * 32 + col], 1u);
+            const uint32_t pos = atomicAdd(&ucnt[slot], 1u);
             if (pos < (uint32_t)CAP)  // always true (flush_at + MARGIN <= CAP): a guard only
               st64(ubuf + pos, dr::make_key(v, gbase + (uint32_t)row));
           }
@@ -698,18 +718,19 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       DG_ADD(kDgDrain, t_d);
       DG_CNT(kDgNDrain);
     };
-    auto stage_hits = [&](int t, f32x16 (&acc)[NU_T], uint32_t hit_bits) {
+    auto stage_hits = [&](int t, f32x16 (&acc)[NG], uint32_t hit_bits, auto GI) {
+      constexpr int g0 = decltype(GI)::value * NG;
       DG_T0(t_e);
       const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
       const int valid = (int)((i_end - tile0) < kTileItems ? (i_end - tile0) : kTileItems);
       const uint32_t gbase = (uint32_t)(a.item_base + tile0);
 #pragma unroll
-      for (int ut = 0; ut < NU_T; ++ut) {
+      for (int ut = 0; ut < NG; ++ut) {
         if (!(hit_bits & (1u << ut))) continue;
         float m = acc[ut][0];
 #pragma unroll
         for (int r = 1; r < 16; ++r) m = fmaxf(m, acc[ut][r]);
-        const bool hit = m > thr[ut];
+        const bool hit = m > thr[g0 + ut];
         const uint64_t bal = __ballot(hit);
         if (bal == 0ull) continue;
         const int n = __popcll(bal);
@@ -722,42 +743,51 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
             dst[q] = make_float4(acc[ut][4 * q], acc[ut][4 * q + 1], acc[ut][4 * q + 2],
                                  acc[ut][4 * q + 3]);
           blk_gbase[i] = gbase;
-          blk_slot[i] = (uint32_t)(ut * 32 + col) | ((uint32_t)h << 16) | ((uint32_t)valid << 17);
-          blk_thr[i] = thr[ut];
+          blk_slot[i] =
+              (uint32_t)((g0 + ut) * 32 + col) | ((uint32_t)h << 16) | ((uint32_t)valid << 17);
+          blk_thr[i] = thr[g0 + ut];
         }
         nblk += n;
       }
       DG_ADD(kDgEnqueue, t_e);
       DG_CNT(kDgNEnqueue);
     };
-    auto epilogue = [&](int t, f32x16 (&acc)[NU_T]) {
+    auto epilogue = [&](int t, f32x16 (&acc)[NG], auto GI) {
       DG_T0(t_h);
-      uint32_t hit_bits = any_hits(acc);
+      uint32_t hit_bits = any_hits(acc, GI);
       DG_ADD(kDgHits, t_h);
       hit_bits = __builtin_amdgcn_readfirstlane(hit_bits);  // ballots: uniform
+      // the stage-end work runs after the last group of the tile
+      constexpr bool last_group = decltype(GI)::value == NGRP - 1;
       if constexpr (STAGED) {
-        if (hit_bits != 0u) stage_hits(t, acc, hit_bits);
+        if (hit_bits != 0u) stage_hits(t, acc, hit_bits, GI);
         // end of a stage: resolve the staged blocks, compact full buffers
-        if ((t + 1) % SR == 0 || t + 1 == ntiles) {
+        if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) {
           if (nblk > 0) resolve();
           check_compact();
         }
       } else {
-        if (hit_bits != 0u) enqueue(t, acc, hit_bits);
+        if (hit_bits != 0u) enqueue(t, acc, hit_bits, GI);
         // end of a stage: compact the buffers that passed flush_at
-        if ((t + 1) % SR == 0 || t + 1 == ntiles) check_compact();
+        if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) check_compact();
       }
     };
     // One accumulator set: the partner wave on the same SIMD issues its MFMAs
     // while this wave runs the epilogue (two waves per SIMD by design).
-    f32x16 acc[NU_T];
+    f32x16 acc[NG];
     for (int t = 0; t < ntiles; ++t) {
       DG_CNT(kDgNTiles);
       if (t % SR == 0) boundary(t / SR);
       DG_T0(t_m);
-      mma_tile(t, acc);
+      mma_tile(t, acc, IC<0>{});
       DG_ADD(kDgMma, t_m);
-      epilogue(t, acc);
+      epilogue(t, acc, IC<0>{});
+      if constexpr (NGRP > 1) {
+        DG_T0(t_m2);
+        mma_tile(t, acc, IC<1>{});
+        DG_ADD(kDgMma, t_m2);
+        epilogue(t, acc, IC<1>{});
+      }
     }
     wait_vmcnt<0>();
     wave_lds_sync();
@@ -768,7 +798,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
 #ifdef DR_TOPK_DIAG
   DG_ADD(kDgTotal, t_kernel);
   dg[kDgRealtime] = __builtin_amdgcn_s_memrealtime() - rt_kernel;
-  if (lane == 0) {
+  if (lane == 0 && a.diag) {  // the rescan (usually empty) leaves the main scan's record
     uint64_t* o = a.diag + ((size_t)blockIdx.x * kWaves + wave) * kDgSlots;
 #pragma unroll
     for (int i = 0; i < kDgSlots; ++i) o[i] = dg[i];
@@ -1279,6 +1309,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   af.user_ids = frows;
   af.pos_map = fpos;
   af.n_users_dev = fcnt;
+  af.diag = nullptr;
   launch_scan<false>(p, af, d, s);
   DR_CHECK_LAUNCH();
 #define DR_FIN_RESCAN(PP) DR_FIN(PP, fpos, fcnt, nullptr)

@@ -136,8 +136,9 @@ def test_score_topk_chunked_catalog_exact():
 def test_score_topk_guess_rescan_exact():
     """Catalogs >= 2^18 rows start from a threshold guessed on a strided sample
     (every 32nd row) and rescan users the guess failed. Here the sampled rows
-    0, 32, ... 288 are "hot": the best items of every non-negative user (group
-    A), so A's guess admits only those 10 items (< k) and all of A must be
+    0, 32, ... 608 are "hot": the best items of every non-negative user (group
+    A). The guess's rank in the sample is ks = 13 for k = 50, so A's guessed
+    threshold is the hot score, it admits only those 20 items (< k) and all of A must be
     rescanned; non-positive users (group B) rank them last and are not. With
     duplicate / permuted user ids and exclusions (some hot items excluded)
     the lists must equal the oracle's exactly."""
@@ -145,7 +146,7 @@ def test_score_topk_guess_rescan_exact():
     d, ni, k = 64, (1 << 18) + 123, 50
     U = np.concatenate([_int_table(rng, 48, d, 0, 3), _int_table(rng, 48, d, -3, 0)])
     I = _int_table(rng, ni, d)
-    I[np.arange(10) * 32] = 3.0  # hot sample rows
+    I[np.arange(20) * 32] = 3.0  # hot sample rows
     users = np.concatenate([rng.permutation(96), rng.integers(0, 96, 24)]).astype(np.int64)
     frozen = [rng.choice(ni, size=rng.integers(0, 50), replace=False) for _ in users]
     for n in range(0, len(users), 4):
@@ -154,6 +155,56 @@ def test_score_topk_guess_rescan_exact():
     s, it = ops.score_topk(_bf16(U), _bf16(I), k, user_ids=torch.from_numpy(users).to(DEV),
                            exclude=(torch.from_numpy(rowptr).to(DEV), torch.from_numpy(cols).to(DEV)))
     ref_i, ref_s = oracle.recommend_topk(U, I, k, users=users, frozen=frozen, return_scores=True)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy(), ref_s)
+
+
+@pytest.mark.parametrize("d", [32, 64, 128])
+def test_score_topk_many_workgroups_exact(d):
+    """More users than one workgroup holds (2048 at d <= 64, 1024 at d = 128):
+    several user blocks, the last one partial."""
+    rng = np.random.default_rng(500 + d)
+    nu, ni, k = 4100 + d, 1500 + 7, 10
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    s, it = ops.score_topk(_bf16(U), _bf16(I), k)
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, return_scores=True)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy(), ref_s)
+
+
+def _exact_topk_torch(U, I, k, block=256):
+    """Integer-valued tables: fp32 scores are exact, so a stable descending
+    sort over ascending item ids IS the (score desc, id asc) order. Used where
+    the per-user oracle loop would take minutes; it is pinned to the oracle by
+    test_score_topk_integer_exact's cases."""
+    Ud = torch.from_numpy(U).to(DEV)
+    Id = torch.from_numpy(I).to(DEV)
+    outs, outi = [], []
+    for b in range(0, Ud.shape[0], block):
+        S = Ud[b:b + block] @ Id.T
+        v, i = torch.sort(S, dim=1, descending=True, stable=True)
+        outs.append(v[:, :k].cpu())
+        outi.append(i[:, :k].cpu())
+    return torch.cat(outi).numpy().astype(np.int64), torch.cat(outs).numpy()
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_score_topk_guess_rescan_many_units_exact(d):
+    """Every user fails the guess (hot sampled rows) and there are more of
+    them than one workgroup holds: the device-counted rescan runs several
+    user blocks, the last one partial, and writes each list to its position."""
+    rng = np.random.default_rng(88 + d)
+    ni, k = (1 << 18) + 77, 20
+    nu = 2 * (2048 if d <= 64 else 1024) + 333
+    U = _int_table(rng, nu, d, 0, 3)
+    I = _int_table(rng, ni, d)
+    # 12 hot sample rows: the best items of every (non-negative) user. The
+    # guess's rank in the sample is ks = ceil(mu + 6 sqrt(mu) + 3) = 9 for
+    # k = 20 (mu = k / 32), so the guessed threshold is the hot score and only
+    # the 12 hot items (< k) pass it: every user fails and is rescanned.
+    I[np.arange(12) * 32] = 3.0
+    s, it = ops.score_topk(_bf16(U), _bf16(I), k)
+    ref_i, ref_s = _exact_topk_torch(U, I, k)
     assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
     assert np.array_equal(s.cpu().numpy(), ref_s)
 
