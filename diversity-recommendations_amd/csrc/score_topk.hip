@@ -100,6 +100,9 @@ enum {
 // at d=128)
 #define DR_ENQ_STAGED 2
 #endif
+#ifndef DR_ENQ_FAST
+#define DR_ENQ_FAST 1  // direct enqueue: one-survivor lanes store their max (no value select)
+#endif
 #ifndef DR_STAGE_BLOCKS
 #define DR_STAGE_BLOCKS 64  // staged lane blocks per wave (>= 64: one user tile always fits)
 #endif
@@ -620,6 +623,27 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         mask &= vmask;
         const int slot = (g0 + ut) * 32 + col;
         uint64_t* ubuf = cbase + (size_t)slot * CAP;  // this lane's user buffer
+#if DR_ENQ_FAST
+        // Common case: every hitting lane holds ONE survivor. It is then the
+        // lane's maximum (all other scores are <= thr < it), so one round
+        // stores it without the 16-way value select. Full tiles only (the
+        // max of a partial tile may sit in a row past the slice end).
+        if (vmask == 0xffffu && __ballot((mask & (mask - 1u)) != 0u) == 0ull) {
+          if (__ballot(mask != 0u) != 0ull) {
+            float m = acc[ut][0];
+#pragma unroll
+            for (int q = 1; q < 16; ++q) m = fmaxf(m, acc[ut][q]);
+            if (mask != 0u) {
+              const int r = __builtin_ctz(mask);
+              const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+              const uint32_t pos = atomicAdd(&ucnt[slot], 1u);
+              if (pos < (uint32_t)CAP) st64(ubuf + pos, dr::make_key(m, gbase + (uint32_t)row));
+            }
+            vmc += 1;  // the store above issued once (some lane had a key)
+          }
+          continue;
+        }
+#endif
         while (__ballot(mask != 0u) != 0ull) {
           const bool has = mask != 0u;
           const int r = has ? __builtin_ctz(mask) : 0;
