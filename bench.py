@@ -67,6 +67,13 @@ def parse():
     ap.add_argument("--item-shards", type=int, default=0,
                     help="ranks that row-shard the item table per user slice (0 = auto: "
                          "2 for an even world size, else the world size)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend (gloo: multi-rank rehearsal on one GPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (rehearsing N ranks on a one-GPU box)")
+    ap.add_argument("--check-users", type=int, default=0,
+                    help="after timing, recompute this many of each rank's final users "
+                         "over the whole catalog on one device and require identical lists")
     ap.add_argument("--workload", default="catalog",
                     choices=["catalog", "score1m", "gather", "bpr", "mmr"])
     return ap.parse_args()
@@ -230,11 +237,15 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = 0 if args.same_device else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     S = 1
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         S = args.item_shards or (2 if world % 2 == 0 else world)
     lay = grid_layout(S) if world > 1 else None
 
@@ -283,7 +294,8 @@ def main():
     dt = time.perf_counter() - t0
     topk_s = sum(a.elapsed_time(b) for a, b in zip(ev["topk0"], ev["topk1"])) / 1e3 / args.steps
     ild_s = sum(a.elapsed_time(b) for a, b in zip(ev["ild0"], ev["ild1"])) / 1e3 / args.steps
-    t = torch.tensor([dt, ild_s], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt, ild_s], dtype=torch.float64,
+                     device="cpu" if args.backend == "gloo" else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, ild_max = float(t[0]), float(t[1])
@@ -330,6 +342,8 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if args.check_users > 0:
+        result["check"] = check_lists(args, lay, users, items, recs, u_lo, U_n, k, world)
     if rank == 0:
         with_measured(result["roofline"], dev, "mfma_bf16_tflops")
     if world == 1 and not args.no_cpu_baseline:
@@ -338,6 +352,30 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def check_lists(args, lay, users, items, recs, u_lo, U_n, k, world):
+    """Multi-rank parity (outside the timed region): the first --check-users
+    users this rank owns after the exchange, rescored over the WHOLE catalog
+    by one score_topk call, must give the identical lists (the key order is
+    total, so any item partition merges bit-identically)."""
+    n_slice = users.shape[0]
+    if lay is not None and lay.item_shards > 1:
+        f_lo, f_hi = shard_range(n_slice, lay.item_shards, lay.item_shard)
+    else:
+        f_lo, f_hi = 0, n_slice
+    n = min(args.check_users, f_hi - f_lo)
+    _, ref = ops.score_topk(users[f_lo:f_lo + n].contiguous(), items, k)
+    ok = bool(torch.equal(ref.to(recs.dtype), recs[:n]))
+    t = torch.tensor([0 if ok else 1, n], dtype=torch.int64, device=users.device)
+    if world > 1:
+        if args.backend == "gloo":
+            t = t.cpu()
+        dist.all_reduce(t)
+    if int(t[0]) != 0:
+        raise SystemExit(f"multi-rank check FAILED on {int(t[0])} rank(s)")
+    return {"users_checked": int(t[1]), "identical": True,
+            "first_user": u_lo + f_lo}
 
 
 # --------------------------------------------------------------------------- secondary workloads

@@ -94,9 +94,15 @@ def exchange_partials(scores: torch.Tensor, items: torch.Tensor, group=None) -> 
     in_splits = [shard_range(n, world, p)[1] - shard_range(n, world, p)[0] for p in range(world)]
     lo, hi = shard_range(n, world, rank)
     n_r = hi - lo
-    out = torch.empty((world * n_r, 2 * k), dtype=torch.int32, device=scores.device)
-    dist.all_to_all_single(out, packed, output_split_sizes=[n_r] * world,
+    # gloo (CPU tests, the one-GPU multi-rank rehearsal) exchanges host
+    # tensors; RCCL exchanges the device tensors in place over xGMI
+    staged = packed.is_cuda and dist.get_backend(group) == "gloo"
+    src = packed.cpu() if staged else packed
+    out = torch.empty((world * n_r, 2 * k), dtype=torch.int32, device=src.device)
+    dist.all_to_all_single(out, src, output_split_sizes=[n_r] * world,
                            input_split_sizes=in_splits, group=group)
+    if staged:
+        out = out.to(scores.device)
     out = out.view(world, n_r, k, 2)
     return out[..., 0].contiguous().view(torch.float32), out[..., 1].contiguous()
 
