@@ -215,16 +215,19 @@ def with_measured(roof: dict, dev, key: str) -> dict:
 
 
 def load_traffic(cfg_key: str):
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        with open(path) as f:
-            rec = json.load(f)
-        if rec.get("config") == cfg_key:
-            return rec.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+    """HBM bytes per dr_score_topk call from a committed PMC summary
+    (tools/gpu_pmc.sh + tools/pmc_traffic.py) for exactly this config."""
+    for name in ("pmc_traffic.json", f"pmc_traffic_{cfg_key}.json"):
+        path = os.path.join(ROOT, "profiles", name)
+        if not os.path.exists(path):
+            continue
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+            if rec.get("config") == cfg_key:
+                return rec.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
     return None
 
 
@@ -446,7 +449,8 @@ def secondary(args):
                "items": I_n, "dim": d, "k": k},
               {"bound": "mfma", "achieved": flops / dt / 1e12, "peak": MFMA_BF16_PEAK_TFLOPS,
                "unit": "TFLOP/s", "frac": flops / dt / 1e12 / MFMA_BF16_PEAK_TFLOPS,
-               "traffic": None, "kernel": "dr_score_topk"}, cpu)
+               "traffic": load_traffic(f"U{U_n}_I{I_n}_d{d}_k{k}_G1"),
+               "kernel": "dr_score_topk (sample scan + thresholds + seeded scan + finalize)"}, cpu)
         return 0
 
     if args.workload == "gather":

@@ -17,7 +17,8 @@ import json
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("score_scan_kernel", "topk_threshold_kernel", "topk_finalize_kernel")
+KERNELS = ("score_scan_kernel", "sample_rows_kernel", "topk_threshold_kernel",
+           "topk_finalize_kernel")
 
 
 def per_kernel(path, counter):
