@@ -1088,7 +1088,10 @@ struct Guess {
 #ifndef DR_GUESS_SIGMA
 #define DR_GUESS_SIGMA 6.0
 #endif
-constexpr int64_t kGuessStride = 32;
+#ifndef DR_GUESS_STRIDE
+#define DR_GUESS_STRIDE 32
+#endif
+constexpr int64_t kGuessStride = DR_GUESS_STRIDE;
 constexpr int64_t kGuessMinItems = 1 << 18;
 #ifndef DR_GUESS_MAX_LOG2
 #define DR_GUESS_MAX_LOG2 23  // measured: +1.7 % at 5M rows, -0.3 % at 10M
