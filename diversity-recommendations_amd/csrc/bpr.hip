@@ -114,7 +114,62 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float* __restrict__ param,
   }
 }
 
+// Row-sparse ("lazy") Adam over the listed rows only: the update
+// torch.optim.SparseAdam applies (torch/optim/_functional.py sparse_adam) to a
+// coalesced sparse gradient whose indices are `rows`, with the values read
+// from the dense gradient table the BPR kernel accumulated. Same fp32 rounding
+// sequence as torch's sequence of tensor ops:
+//   u1 = (g - m) * w1;  m' = m + u1
+//   u2 = (g * g - v) * w2;  v' = v + u2
+//   p' = p + neg_step * ((u1 + m) / (sqrt(u2 + v) + eps))
+// The touched gradient entries are zeroed afterwards (zero_grad of the rows),
+// so the dense gradient table never needs a full memset. One thread per
+// element: rows are contiguous, so a wave covers 64 consecutive floats.
+__global__ __launch_bounds__(kBlock) void adam_rows_kernel(
+    float* __restrict__ param, float* __restrict__ grad, float* __restrict__ m,
+    float* __restrict__ v, int64_t d, const int64_t* __restrict__ rows, int64_t n,
+    float w1, float w2, float neg_step, float eps, int zero_grad) {
+#pragma clang fp contract(off)
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const int64_t r = i / d;
+    const int64_t e = rows[r] * d + (i - r * d);
+    const float g = grad[e];
+    const float mo = m[e], vo = v[e];
+    const float u1 = (g - mo) * w1;
+    const float u2 = (g * g - vo) * w2;
+    m[e] = mo + u1;
+    v[e] = vo + u2;
+    const float q = (u1 + mo) / (sqrtf(u2 + vo) + eps);
+    param[e] = param[e] + neg_step * q;
+    if (zero_grad) grad[e] = 0.f;
+  }
+}
+
 }  // namespace
+
+extern "C" int dr_adam_rows(float* param, float* grad, float* exp_avg, float* exp_avg_sq,
+                            int64_t d, const int64_t* rows, int64_t n_rows, double lr,
+                            double beta1, double beta2, double eps, int64_t step, int zero_grad,
+                            dr_stream_t stream) {
+  DR_CHECK_ARG(n_rows >= 0 && d >= 1 && step >= 1, "n_rows must be >= 0, d >= 1, step >= 1");
+  if (n_rows == 0) return DR_OK;
+  DR_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && rows, "null pointer");
+  // Python-float arithmetic of sparse_adam, in double, cast once:
+  // step_size = lr * sqrt(1 - beta2^step) / (1 - beta1^step); mul by -step_size.
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  const double step_size = lr * std::sqrt(bc2) / bc1;
+  const int64_t n = n_rows * d;
+  int64_t grid = dr::ceil_div(n, kBlock);
+  if (grid > 256 * 16) grid = 256 * 16;
+  hipLaunchKernelGGL(adam_rows_kernel, dim3((unsigned)grid), dim3(kBlock), 0,
+                     (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq, d, rows, n,
+                     (float)(1.0 - beta1), (float)(1.0 - beta2), (float)(-step_size), (float)eps,
+                     zero_grad);
+  DR_CHECK_LAUNCH();
+  return DR_OK;
+}
 
 extern "C" int dr_bpr_fwd_bwd(const float* user_table, const float* item_table, int64_t d,
                               const int64_t* user_id, const int64_t* pos_id,

@@ -281,6 +281,29 @@ def adam_dense(
     B.check(rc, "dr_adam_dense")
 
 
+def adam_rows(
+    param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
+    rows: torch.Tensor, lr: float, beta1: float, beta2: float, eps: float, step: int,
+    zero_grad: bool = True,
+) -> None:
+    """torch.optim.SparseAdam's update over the UNIQUE rows ``rows`` of 2-D
+    fp32 tables (gradient values read from the dense ``grad``); with
+    ``zero_grad`` the touched gradient rows are zeroed afterwards."""
+    dev = B.require_device(param, grad, exp_avg, exp_avg_sq, rows)
+    _need(param.dim() == 2, "adam_rows: param must be a 2-D table")
+    for t in (param, grad, exp_avg, exp_avg_sq):
+        _need(t.dtype == torch.float32 and t.is_contiguous() and t.shape == param.shape,
+              "adam_rows tensors must be contiguous fp32 tables of equal shape")
+    rows = rows.to(torch.int64).contiguous()
+    _need(rows.dim() == 1, "adam_rows: rows must be 1-D")
+    rc = B.lib().dr_adam_rows(
+        param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+        param.size(1), rows.data_ptr(), rows.numel(), float(lr), float(beta1), float(beta2),
+        float(eps), int(step), 1 if zero_grad else 0, B.stream(dev),
+    )
+    B.check(rc, "dr_adam_rows")
+
+
 # --------------------------------------------------------------------------- catalog histogram
 def catalog_histogram(recs: torch.Tensor, n_items: int) -> Tuple[torch.Tensor, torch.Tensor]:
     """(counts int32 [n_items], position sums int64 [n_items]) of the item ids

@@ -156,6 +156,35 @@ def fused_adam_step(optimizer: torch.optim.Adam) -> None:
                            beta2, group["eps"], group["weight_decay"], int(st["step"].item()))
 
 
+def _plain_sparse_adam(optimizer: torch.optim.Optimizer) -> bool:
+    return type(optimizer) is torch.optim.SparseAdam and not any(
+        g.get("maximize") for g in optimizer.param_groups)
+
+
+def lazy_adam_step(optimizer: torch.optim.SparseAdam, rows: dict) -> None:
+    """optimizer.step() of torch.optim.SparseAdam done by dr_adam_rows on the
+    optimizer's own state: for each parameter p, ``rows[p]`` holds the unique
+    rows the batch touched (the indices a sparse embedding gradient would
+    carry). The reference's embeddings are dense (sparse=False), so plain
+    torch cannot run SparseAdam on them; this is the opt-in row-sparse
+    ("lazy") alternative to dense Adam. The touched
+    gradient rows are zeroed, so the dense gradient tables stay allocated and
+    all-zero between batches (no full memset, no re-allocation)."""
+    for group in optimizer.param_groups:
+        beta1, beta2 = group["betas"]
+        for p in group["params"]:
+            if p.grad is None or p not in rows:
+                continue
+            st = optimizer.state[p]
+            if len(st) == 0:
+                st["step"] = 0
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["step"] += 1
+            ops.adam_rows(p.data, p.grad, st["exp_avg"], st["exp_avg_sq"], rows[p],
+                          group["lr"], beta1, beta2, group["eps"], st["step"])
+
+
 def _bpr_fast_path(model, loss, scores) -> bool:
     return (isinstance(model, MatrixFactorization) and type(loss) is LogSigmoidDifferenceLoss
             and (scores is None or all(type(s) is AUCScore for s in scores)))
@@ -172,6 +201,7 @@ def pair_wise_train_loop(dataset: PairWiseDataset, model: RankingModel, loss: Pa
     batch_losses, batch_scores = [], []
     fused = _bpr_fast_path(model, loss, scores)
     adam = _plain_adam(optimizer)
+    lazy = fused and _plain_sparse_adam(optimizer)
     for user_id, pos, neg, uf, pf, nf in dataset.loader(**loader_params):
         if fused:
             dev = model._device()
@@ -184,11 +214,15 @@ def pair_wise_train_loop(dataset: PairWiseDataset, model: RankingModel, loss: Pa
             B = uid.numel()
             losses_b, hits = ops.bpr_fwd_bwd(U.data, I.data, uid, pid, nid, 1.0 / B, U.grad, I.grad)
             loss_value = torch.sum(losses_b, dim=0) / B
-            if adam:
+            if lazy:  # touched rows only; the kernel zeroes those gradient rows
+                lazy_adam_step(optimizer, {U: torch.unique(uid),
+                                           I: torch.unique(torch.cat([pid, nid]))})
+            elif adam:
                 fused_adam_step(optimizer)
+                optimizer.zero_grad()
             else:
                 optimizer.step()
-            optimizer.zero_grad()
+                optimizer.zero_grad()
             batch_losses.append(loss_value.detach())
             if n_scores:
                 auc = torch.sum(hits.float(), dim=0) / B

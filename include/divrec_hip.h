@@ -157,6 +157,20 @@ int dr_adam_dense(float* param, const float* grad, float* exp_avg, float* exp_av
                   int64_t n, double lr, double beta1, double beta2, double eps,
                   double weight_decay, int64_t step, dr_stream_t stream);
 
+/* Row-sparse ("lazy") Adam, SURVEY.md §8f rank 3: the update
+ * torch.optim.SparseAdam applies (torch/optim/_functional.py, sparse_adam) to
+ * a coalesced sparse gradient with indices `rows` (unique, int64, [n_rows]) and
+ * values grad[rows] read from a DENSE fp32 gradient table [*, d] (as
+ * accumulated by dr_bpr_fwd_bwd). Only the listed rows of param / exp_avg /
+ * exp_avg_sq change. zero_grad != 0 also zeroes grad[rows], leaving the table
+ * all-zero for the next batch without a full memset. The reference trains with
+ * dense Adam (divrec/train/utils.py:151 over sparse=False embeddings,
+ * divrec/models/matrix_factorization.py:16-17); this is the opt-in alternative.
+ * `step` is SparseAdam's state step AFTER incrementing. */
+int dr_adam_rows(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t d,
+                 const int64_t* rows, int64_t n_rows, double lr, double beta1, double beta2,
+                 double eps, int64_t step, int zero_grad, dr_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Accuracy metrics of top-k lists against test interactions, per user
  * (SURVEY.md §8f rank 1): precision@k (divrec/metrics/precision_at_k.py:6-22),

@@ -261,3 +261,101 @@ def test_score_topk_api_exclusion_and_user_subset():
                                                              torch.from_numpy(cols)))
     ref = oracle.recommend_topk(U[10:30], I, 25, frozen=frozen)
     assert np.array_equal(items.cpu().numpy(), ref)
+
+
+# --------------------------------------------------------------------------- lazy (row-sparse) Adam
+def _sparse_adam_reference(P0, steps, lr, betas, eps):
+    """torch.optim.SparseAdam on the CPU, fp32: steps = [(rows, grad_values)]."""
+    p = torch.nn.Parameter(torch.from_numpy(P0.copy()))
+    opt = torch.optim.SparseAdam([p], lr=lr, betas=betas, eps=eps)
+    for rows, vals in steps:
+        p.grad = torch.sparse_coo_tensor(torch.from_numpy(rows)[None, :], torch.from_numpy(vals),
+                                         P0.shape).coalesce()
+        opt.step()
+    st = opt.state[p]
+    return p.detach().numpy(), st["exp_avg"].numpy(), st["exp_avg_sq"].numpy()
+
+
+def test_adam_rows_vs_torch_sparse_adam():
+    """dr_adam_rows over three steps with different row sets, against
+    (1) the oracle's restatement of SparseAdam's fp32 op sequence with IEEE
+    sqrt / division: bit-exact for param, exp_avg, exp_avg_sq;
+    (2) torch.optim.SparseAdam on the CPU: exp_avg / exp_avg_sq bit-exact,
+    param within 1e-6 (torch's CPU vector sqrt is not correctly rounded: the
+    last bit differs for ~0.7 % of inputs). Untouched rows keep their values
+    and the touched gradient rows are zeroed."""
+    rng = np.random.default_rng(31)
+    n, d, lr, betas, eps = 500, 100, 3e-3, (0.85, 0.995), 1e-7
+    P0 = rng.standard_normal((n, d)).astype(np.float32)
+    steps = []
+    for _ in range(3):
+        rows = np.sort(rng.choice(n, size=137, replace=False)).astype(np.int64)
+        vals = (rng.standard_normal((rows.size, d)) * 0.1).astype(np.float32)
+        steps.append((rows, vals))
+    refP, refM, refV = _sparse_adam_reference(P0, steps, lr, betas, eps)
+    oP, oM, oV = P0.copy(), np.zeros_like(P0), np.zeros_like(P0)
+    for t, (rows, vals) in enumerate(steps, start=1):
+        oracle.sparse_adam_rows(oP, oM, oV, rows, vals, t, lr, *betas, eps)
+    P = torch.from_numpy(P0).to(DEV)
+    M, V = torch.zeros_like(P), torch.zeros_like(P)
+    G = torch.zeros_like(P)
+    for t, (rows, vals) in enumerate(steps, start=1):
+        r = torch.from_numpy(rows).to(DEV)
+        G[r] = torch.from_numpy(vals).to(DEV)
+        ops.adam_rows(P, G, M, V, r[torch.randperm(r.numel(), device=DEV)], lr, *betas, eps, t)
+        assert int(torch.count_nonzero(G)) == 0  # touched rows zeroed, the rest stayed zero
+    assert np.array_equal(P.cpu().numpy(), oP)
+    assert np.array_equal(M.cpu().numpy(), oM)
+    assert np.array_equal(V.cpu().numpy(), oV)
+    assert np.array_equal(M.cpu().numpy(), refM)
+    assert np.array_equal(V.cpu().numpy(), refV)
+    assert np.allclose(P.cpu().numpy(), refP, rtol=0, atol=1e-6)
+
+
+def test_pair_wise_train_loop_sparse_adam():
+    """pair_wise_train_loop with torch.optim.SparseAdam takes the fused BPR
+    kernel + dr_adam_rows path. Reference: the same batches through an
+    nn.Embedding(sparse=True) copy of the model and torch's SparseAdam on the
+    CPU. Gradients differ only by the fp32 atomic summation order (rel 1e-5),
+    so the parameters after the epoch agree within 1e-5."""
+    rng = np.random.default_rng(8)
+    nu, ni, d, lr = 12, 40, 32, 1e-2
+    U0 = rng.standard_normal((nu, d)).astype(np.float32)
+    I0 = rng.standard_normal((ni, d)).astype(np.float32)
+    inter = np.stack([rng.integers(0, nu, 150), rng.integers(0, ni, 150)], axis=1)
+    data = datasets.UserItemInteractionsDataset(
+        torch.from_numpy(inter).long(), number_of_users=nu, number_of_items=ni,
+        user_features=datasets.Features(torch.zeros(nu, 1), ["x"]),
+        item_features=datasets.Features(torch.zeros(ni, 1), ["x"]))
+    random.seed(5)
+    pw = datasets.PairWiseDataset(data, max_sampled=4)
+    batches = [(u.clone(), p.clone(), n.clone()) for u, p, n, *_ in pw.loader(batch_size=64)]
+
+    mf = mf_from(U0, I0)
+    opt = torch.optim.SparseAdam(list(mf.parameters()), lr=lr)
+    random.seed(5)
+    pw = datasets.PairWiseDataset(data, max_sampled=4)
+    mean_loss, (mean_auc,) = train.pair_wise_train_loop(
+        pw, mf, losses.LogSigmoidDifferenceLoss(), opt, scores=[metrics.AUCScore()],
+        batch_size=64)
+
+    Ue = torch.nn.Embedding(nu, d, sparse=True)
+    Ie = torch.nn.Embedding(ni, d, sparse=True)
+    with torch.no_grad():
+        Ue.weight.copy_(torch.from_numpy(U0))
+        Ie.weight.copy_(torch.from_numpy(I0))
+    ref_opt = torch.optim.SparseAdam(list(Ue.parameters()) + list(Ie.parameters()), lr=lr)
+    ref_losses = []
+    for u, p, n in batches:
+        sp = torch.sum(Ue(u) * Ie(p), dim=1)
+        sn = torch.sum(Ue(u) * Ie(n), dim=1)
+        loss = -torch.nn.functional.logsigmoid(sp - sn).mean()
+        loss.backward()
+        ref_opt.step()
+        ref_opt.zero_grad()
+        ref_losses.append(float(loss))
+    assert mean_loss == pytest.approx(sum(ref_losses) / len(ref_losses), rel=1e-5)
+    assert np.allclose(mf.user_embeddings.weight.detach().cpu().numpy(),
+                       Ue.weight.detach().numpy(), rtol=0, atol=1e-5)
+    assert np.allclose(mf.item_embeddings.weight.detach().cpu().numpy(),
+                       Ie.weight.detach().numpy(), rtol=0, atol=1e-5)

@@ -115,3 +115,28 @@ def test_mmr_lambda_one_is_topk():
     assert oracle.mmr_check(got, cand, sc, E, 1.0) == 0
     got5 = oracle.mmr_greedy(cand, sc, E, 10, 0.5)
     assert oracle.mmr_check(got5, cand, sc, E, 0.5) == 0
+
+
+def test_oracle_sparse_adam_rows_vs_torch():
+    """The oracle's SparseAdam restatement (the bit-exact target of
+    dr_adam_rows) against torch.optim.SparseAdam on the CPU: moments bit-exact;
+    the parameter within 1e-6 (torch's CPU vector sqrt is not correctly
+    rounded, the oracle's is)."""
+    import torch
+    rng = np.random.default_rng(12)
+    n, d, lr, betas, eps = 200, 48, 1e-2, (0.9, 0.999), 1e-8
+    P0 = rng.standard_normal((n, d)).astype(np.float32)
+    p = torch.nn.Parameter(torch.from_numpy(P0.copy()))
+    opt = torch.optim.SparseAdam([p], lr=lr, betas=betas, eps=eps)
+    oP, oM, oV = P0.copy(), np.zeros_like(P0), np.zeros_like(P0)
+    for t in range(1, 4):
+        rows = np.sort(rng.choice(n, size=60, replace=False)).astype(np.int64)
+        vals = rng.standard_normal((rows.size, d)).astype(np.float32)
+        p.grad = torch.sparse_coo_tensor(torch.from_numpy(rows)[None, :], torch.from_numpy(vals),
+                                         P0.shape).coalesce()
+        opt.step()
+        oracle.sparse_adam_rows(oP, oM, oV, rows, vals, t, lr, *betas, eps)
+    st = opt.state[p]
+    assert np.array_equal(oM, st["exp_avg"].numpy())
+    assert np.array_equal(oV, st["exp_avg_sq"].numpy())
+    assert np.allclose(oP, p.detach().numpy(), rtol=0, atol=1e-6)
