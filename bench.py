@@ -542,6 +542,21 @@ def secondary(args):
             nrows[0], nrows[1] = ru.numel(), ri.numel()
 
         lwall, _ = _timed(lazy_step, args.steps, args.warmup)
+
+        # device-side PairWiseDataset sampling: m = 20 (the
+        # reference config's train_max_sampled), users in order, ~B triples
+        m_s = 20
+        n_su = B // (m_s * m_s)
+        s_rowptr = torch.arange(0, (U_n + 1) * npos, npos, dtype=torch.int64, device=dev)
+        s_items = pos.reshape(-1).to(torch.int32)
+        s_users = torch.arange(n_su, dtype=torch.int64, device=dev)
+        sw, sdt = _timed(lambda: ops.sample_pairwise(s_users, s_rowptr, s_items, I_n, m_s, 11),
+                         args.steps, args.warmup)
+        sampler = {"value": n_su * m_s * m_s / sw, "unit": "triples/s", "ms_per_call": sw * 1e3,
+                   "users": n_su, "max_sampled": m_s,
+                   "kernel": "dr_sample_pairwise (draw + pos-major expand, one host read of "
+                             "the error counter per call)",
+                   "bytes_per_call": n_su * m_s * m_s * 24}
         tu = sum(a.elapsed_time(b) for a, b in lev["unique"][-args.steps:]) / 1e3 / args.steps
         tr = sum(a.elapsed_time(b) for a, b in lev["rows"][-args.steps:]) / 1e3 / args.steps
         rows_bytes = (nrows[0] + nrows[1]) * (8 * d * 4 + 8)  # p,m,v rw + g read + g zero + id
@@ -582,7 +597,7 @@ def secondary(args):
                "dim": d, "batch": B},
               dict(_hbm(per_triple * B, tb), kernel="dr_bpr_fwd_bwd",
                    per_unit=f"{per_triple} B/triple"),
-              cpu, bpr_ms=tb * 1e3, adam_ms=ta * 1e3, lazy_adam_step=lazy,
+              cpu, bpr_ms=tb * 1e3, adam_ms=ta * 1e3, lazy_adam_step=lazy, sampler=sampler,
               adam_roofline=_hbm(adam_bytes, ta),
               # the fused kernel's real ceiling: fp32 atomics execute at the memory
               # side at ~1.3 TB/s of added bytes chip-wide (MI355X_MICROARCH.md,

@@ -50,6 +50,8 @@ SIGNATURES = {
     "dr_ild_embedding": (_i32, [_p, _i32, _i64, _i32, _p, _i64, _i32, _i32, _p, _p]),
     "dr_bpr_fwd_bwd": (_i32, [_p, _p, _i64, _p, _p, _p, _i64, _f32, _p, _p, _p, _p, _p]),
     "dr_adam_dense": (_i32, [_p, _p, _p, _p, _i64, _f64, _f64, _f64, _f64, _f64, _i64, _p]),
+    "dr_sample_pairwise": (_i32, [_p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_uint64, _p, _p,
+                                  _p, _p, _p, _p, _p]),
     "dr_adam_rows": (_i32, [_p, _p, _p, _p, _i64, _p, _i64, _f64, _f64, _f64, _f64, _i64, _i32,
                             _p]),
     "dr_mmr_rerank": (_i32, [_p, _p, _i64, _i32, _p, _i64, _i32, _i32, _f32, _p, _p]),

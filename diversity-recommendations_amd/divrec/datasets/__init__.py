@@ -1,4 +1,5 @@
 from .base_datasets import (
+    DevicePairWiseDataset,
     PairWiseDataset,
     PairWiseRow,
     PointWiseDataset,
@@ -9,6 +10,7 @@ from .base_datasets import (
 from .storages import Features, UserItemInteractionsDataset
 
 __all__ = [
+    "DevicePairWiseDataset",
     "Features",
     "UserItemInteractionsDataset",
     "PairWiseRow",

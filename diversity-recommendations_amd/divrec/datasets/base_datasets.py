@@ -120,3 +120,74 @@ class RankingDataset(IterableDataset):
         if self.frozen is None or not self.frozen.has_interactions():
             return None
         return self.frozen.user_item_csr(self.data.number_of_users)
+
+
+def _device_csr(data: UserItemInteractionsDataset, n_users: int, n_items: int, device):
+    """Unique (user, item) pairs of ``data`` as a CSR on ``device``: rowptr
+    int64 [n_users + 1], items int32 sorted per user (frozenset semantics)."""
+    inter = data.interactions.to(device=device, dtype=torch.int64)
+    key = torch.unique(inter[:, 0] * n_items + inter[:, 1])  # sorted, unique
+    users, items = key // n_items, key % n_items
+    counts = torch.bincount(users, minlength=n_users)
+    rowptr = torch.zeros(n_users + 1, dtype=torch.int64, device=device)
+    rowptr[1:] = torch.cumsum(counts, 0)
+    return rowptr, items.to(torch.int32).contiguous()
+
+
+class DevicePairWiseDataset:
+    """PairWiseDataset with the sampling on the GPU.
+
+    Same populations, layout and order as the reference's PairWiseDataset
+    (base_datasets.py:70-107): users 0..U-1, per user m positives drawn with
+    replacement from its unique positives and m negatives from
+    items - positives - frozen, yielded as the m x m product (positive-major).
+    The draws come from dr_sample_pairwise's counter-based generator instead of
+    Python's ``random`` (parity is distributional; each ``loader()`` call is a
+    new epoch with fresh draws). ``loader(batch_size=B)`` yields batches of B
+    consecutive triples as device tensors ``(user, positive, negative, None,
+    None, None)`` (features are not gathered: the MF fast path ignores them).
+    Requires ``max_sampled > 0``. A user without positives raises IndexError,
+    as the reference does, when its chunk is sampled."""
+
+    def __init__(self, data: UserItemInteractionsDataset,
+                 frozen: Optional[UserItemInteractionsDataset] = None, max_sampled: int = 100,
+                 device="cuda", seed: int = 0, triples_per_chunk: int = 1 << 22):
+        if max_sampled <= 0:
+            raise ValueError("DevicePairWiseDataset samples: max_sampled must be > 0")
+        self.data = data
+        self.frozen = frozen
+        self.max_sampled = int(max_sampled)
+        self.device = torch.device(device)
+        self.seed = int(seed)
+        self.epoch = 0
+        self.n_users = int(data.number_of_users)
+        self.n_items = int(data.number_of_items)
+        self.pos_csr = _device_csr(data, self.n_users, self.n_items, self.device)
+        self.excl_csr = None
+        if frozen is not None:
+            self.excl_csr = _device_csr(frozen, self.n_users, self.n_items, self.device)
+        self.users_per_chunk = max(1, triples_per_chunk // (self.max_sampled ** 2))
+
+    def __len__(self) -> int:
+        return self.n_users * self.max_sampled ** 2
+
+    def loader(self, batch_size: int = 1, **_unused) -> Iterator[PairWiseRow]:
+        from .. import ops  # device path only
+
+        seed = (self.seed * 0x9E3779B97F4A7C15 + self.epoch) & ((1 << 64) - 1)
+        self.epoch += 1
+        carry = None
+        for u0 in range(0, self.n_users, self.users_per_chunk):
+            users = torch.arange(u0, min(u0 + self.users_per_chunk, self.n_users),
+                                 dtype=torch.int64, device=self.device)
+            _, _, trip = ops.sample_pairwise(users, *self.pos_csr, self.n_items, self.max_sampled,
+                                             seed, exclude=self.excl_csr)
+            if carry is not None:
+                trip = tuple(torch.cat([c, t]) for c, t in zip(carry, trip))
+            n_full = trip[0].numel() // batch_size * batch_size
+            for b0 in range(0, n_full, batch_size):
+                yield (trip[0][b0:b0 + batch_size], trip[1][b0:b0 + batch_size],
+                       trip[2][b0:b0 + batch_size], None, None, None)
+            carry = tuple(t[n_full:] for t in trip)
+        if carry is not None and carry[0].numel() > 0:
+            yield carry[0], carry[1], carry[2], None, None, None

@@ -304,6 +304,41 @@ def adam_rows(
     B.check(rc, "dr_adam_rows")
 
 
+# --------------------------------------------------------------------------- pairwise sampler
+def sample_pairwise(users: torch.Tensor, pos_rowptr: torch.Tensor, pos_items: torch.Tensor,
+                    n_items: int, m: int, seed: int,
+                    exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                    expand: bool = True):
+    """PairWiseDataset's per-user sampling on the device (dr_sample_pairwise).
+    Returns (pos [n, m] int32, neg [n, m] int32, triples) where triples is
+    (uid, pid, nid) int64 [n*m*m] in the reference's pos-major order, or None
+    without ``expand``. Raises IndexError, as the reference does, when a user
+    has no positives or no allowed negative (this reads one device counter)."""
+    dev = B.require_device(users, pos_rowptr, pos_items)
+    _need(pos_items.dtype == torch.int32 and pos_rowptr.dtype == torch.int64,
+          "positives CSR must be int64 rowptr / int32 items")
+    users = users.to(torch.int64).contiguous()
+    n = users.numel()
+    pos = torch.empty((n, m), dtype=torch.int32, device=dev)
+    neg = torch.empty((n, m), dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    trip = None
+    if expand:
+        trip = tuple(torch.empty(n * m * m, dtype=torch.int64, device=dev) for _ in range(3))
+    er, ei = (None, None) if exclude is None else exclude
+    rc = B.lib().dr_sample_pairwise(
+        users.data_ptr(), n, pos_rowptr.contiguous().data_ptr(), pos_items.contiguous().data_ptr(),
+        B.ptr(er), B.ptr(ei), int(n_items), int(m), int(seed) & ((1 << 64) - 1),
+        pos.data_ptr(), neg.data_ptr(), *(B.ptr(t) for t in (trip or (None,) * 3)),
+        err.data_ptr(), B.stream(dev),
+    )
+    B.check(rc, "dr_sample_pairwise")
+    if int(err.item()) != 0:
+        raise IndexError("Cannot choose from an empty sequence (a user without positives, "
+                         "or without any allowed negative)")
+    return pos, neg, trip
+
+
 # --------------------------------------------------------------------------- catalog histogram
 def catalog_histogram(recs: torch.Tensor, n_items: int) -> Tuple[torch.Tensor, torch.Tensor]:
     """(counts int32 [n_items], position sums int64 [n_items]) of the item ids

@@ -171,6 +171,26 @@ int dr_adam_rows(float* param, float* grad, float* exp_avg, float* exp_avg_sq, i
                  const int64_t* rows, int64_t n_rows, double lr, double beta1, double beta2,
                  double eps, int64_t step, int zero_grad, dr_stream_t stream);
 
+/* Device-side pairwise sampling, SURVEY.md §8f rank 4: the sampling of
+ * PairWiseDataset.__iter__ (divrec/datasets/base_datasets.py:70-107) for the
+ * users `users` [n_users] (int64 row ids), in that order:
+ *   pos_out[b, :] = m draws with replacement, uniform over the user's unique
+ *                   positives (CSR pos_rowptr [*+1] / pos_items int32, sorted);
+ *   neg_out[b, :] = m draws with replacement, uniform over
+ *                   [0, n_items) - positives - frozen (CSR excl_*, may be NULL),
+ *                   by rejection (at most 4096 tries per draw);
+ *   uid/pid/nid [n_users*m*m] int64 (optional, all or none): the m x m
+ *                   Cartesian product, positive-major, as the reference yields it.
+ * Draws come from a counter-based hash of (seed, user id, draw, try) instead of
+ * Python's random stream: parity is distributional. *err_count (caller-zeroed)
+ * counts failed draws: users without positives (the reference raises
+ * IndexError) and negatives with an empty allowed set; their ids are -1. */
+int dr_sample_pairwise(const int64_t* users, int64_t n_users, const int64_t* pos_rowptr,
+                       const int32_t* pos_items, const int64_t* excl_rowptr,
+                       const int32_t* excl_items, int64_t n_items, int m, uint64_t seed,
+                       int32_t* pos_out, int32_t* neg_out, int64_t* uid, int64_t* pid,
+                       int64_t* nid, int32_t* err_count, dr_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Accuracy metrics of top-k lists against test interactions, per user
  * (SURVEY.md §8f rank 1): precision@k (divrec/metrics/precision_at_k.py:6-22),

@@ -353,9 +353,103 @@ def test_pair_wise_train_loop_sparse_adam():
         loss.backward()
         ref_opt.step()
         ref_opt.zero_grad()
-        ref_losses.append(float(loss))
+        ref_losses.append(float(loss.detach()))
     assert mean_loss == pytest.approx(sum(ref_losses) / len(ref_losses), rel=1e-5)
     assert np.allclose(mf.user_embeddings.weight.detach().cpu().numpy(),
                        Ue.weight.detach().numpy(), rtol=0, atol=1e-5)
     assert np.allclose(mf.item_embeddings.weight.detach().cpu().numpy(),
                        Ie.weight.detach().numpy(), rtol=0, atol=1e-5)
+
+
+# --------------------------------------------------------------------------- device pairwise sampler
+def _sampler_fixture(rng, nu=60, ni=500):
+    inter = np.stack([np.repeat(np.arange(nu), 6), rng.integers(0, ni, nu * 6)], axis=1)
+    inter = np.concatenate([inter, inter[:40]])  # duplicate pairs: frozenset semantics
+    frozen = np.stack([rng.integers(0, nu, 900), rng.integers(0, ni, 900)], axis=1)
+    data = datasets.UserItemInteractionsDataset(torch.from_numpy(inter).long(),
+                                                number_of_users=nu, number_of_items=ni)
+    fz = datasets.UserItemInteractionsDataset(torch.from_numpy(frozen).long(),
+                                              number_of_users=nu, number_of_items=ni)
+    pos = [set(inter[inter[:, 0] == u, 1].tolist()) for u in range(nu)]
+    frz = [set(frozen[frozen[:, 0] == u, 1].tolist()) for u in range(nu)]
+    return data, fz, pos, frz
+
+
+def test_sample_pairwise_layout_membership_determinism():
+    """dr_sample_pairwise vs the reference's PairWiseDataset contract
+    (base_datasets.py:70-107): every positive is one of the user's positives,
+    every negative is outside positives and frozen, triples are the m x m
+    product in positive-major order for users in order; same seed -> same
+    draws, another seed -> other draws."""
+    rng = np.random.default_rng(40)
+    data, fz, pos, frz = _sampler_fixture(rng)
+    m = 16
+    ds = datasets.DevicePairWiseDataset(data, frozen=fz, max_sampled=m, device=DEV, seed=3)
+    users = torch.arange(60, device=DEV)
+    p, n, (uid, pid, nid) = ops.sample_pairwise(users, *ds.pos_csr, 500, m, 77, exclude=ds.excl_csr)
+    p, n = p.cpu().numpy(), n.cpu().numpy()
+    uid, pid, nid = (t.cpu().numpy().reshape(60, m, m) for t in (uid, pid, nid))
+    for u in range(60):
+        assert set(p[u].tolist()) <= pos[u]
+        assert not (set(n[u].tolist()) & (pos[u] | frz[u]))
+        assert n[u].min() >= 0 and n[u].max() < 500
+        assert np.all(uid[u] == u)
+        assert np.array_equal(pid[u], np.repeat(p[u][:, None], m, axis=1))  # positive-major
+        assert np.array_equal(nid[u], np.repeat(n[u][None, :], m, axis=0))
+    p2, n2, _ = ops.sample_pairwise(users, *ds.pos_csr, 500, m, 77, exclude=ds.excl_csr,
+                                    expand=False)
+    assert np.array_equal(p2.cpu().numpy(), p) and np.array_equal(n2.cpu().numpy(), n)
+    p3, n3, _ = ops.sample_pairwise(users, *ds.pos_csr, 500, m, 78, exclude=ds.excl_csr,
+                                    expand=False)
+    assert not np.array_equal(n3.cpu().numpy(), n)
+
+
+def test_sample_pairwise_uniform():
+    """Draws are uniform over the populations random.choices samples: the
+    user's unique positives and items - positives - frozen (chi-square,
+    p > 1e-4 for each)."""
+    from scipy.stats import chisquare
+    ni, m = 400, 40000
+    inter = np.array([[0, i] for i in (3, 9, 9, 27, 100, 250, 399)], dtype=np.int64)
+    frozen = np.array([[0, i] for i in range(150, 200)], dtype=np.int64)
+    data = datasets.UserItemInteractionsDataset(torch.from_numpy(inter), number_of_users=1,
+                                                number_of_items=ni)
+    fz = datasets.UserItemInteractionsDataset(torch.from_numpy(frozen), number_of_users=1,
+                                              number_of_items=ni)
+    ds = datasets.DevicePairWiseDataset(data, frozen=fz, max_sampled=1, device=DEV)
+    p, n, _ = ops.sample_pairwise(torch.zeros(1, dtype=torch.int64, device=DEV), *ds.pos_csr, ni,
+                                  m, 5, exclude=ds.excl_csr, expand=False)
+    p, n = p.cpu().numpy().ravel(), n.cpu().numpy().ravel()
+    P = [3, 9, 27, 100, 250, 399]
+    allowed = sorted(set(range(ni)) - set(P) - set(range(150, 200)))
+    assert set(p.tolist()) == set(P) and set(n.tolist()) <= set(allowed)
+    assert chisquare([np.sum(p == i) for i in P]).pvalue > 1e-4
+    assert chisquare([np.sum(n == i) for i in allowed]).pvalue > 1e-4
+
+
+def test_sample_pairwise_user_without_positives_raises():
+    data = datasets.UserItemInteractionsDataset(torch.tensor([[0, 1], [2, 3]]),
+                                                number_of_users=3, number_of_items=10)
+    ds = datasets.DevicePairWiseDataset(data, max_sampled=2, device=DEV)
+    with pytest.raises(IndexError):  # the reference: random.choices([]) -> IndexError
+        list(ds.loader(batch_size=4))
+
+
+def test_device_pairwise_dataset_trains():
+    """pair_wise_train_loop over DevicePairWiseDataset (fused BPR + fused Adam):
+    every batch but the last has batch_size triples, the loss falls over
+    epochs and AUC rises above chance."""
+    rng = np.random.default_rng(41)
+    data, fz, _, _ = _sampler_fixture(rng)
+    ds = datasets.DevicePairWiseDataset(data, frozen=fz, max_sampled=10, device=DEV, seed=1)
+    sizes = [b[0].numel() for b in ds.loader(batch_size=512)]
+    assert sum(sizes) == 60 * 100 and all(s == 512 for s in sizes[:-1])
+    torch.manual_seed(0)
+    mf = models.MatrixFactorization(60, 500, 32).to(DEV)
+    opt = torch.optim.Adam(mf.parameters(), lr=5e-2)
+    hist = [train.pair_wise_train_loop(ds, mf, losses.LogSigmoidDifferenceLoss(), opt,
+                                       scores=[metrics.AUCScore()], batch_size=512)
+            for _ in range(5)]
+    assert all(np.isfinite(h[0]) for h in hist)
+    assert hist[-1][0] < hist[0][0]
+    assert hist[-1][1][0] > 0.6
