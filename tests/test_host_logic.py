@@ -93,3 +93,25 @@ def test_pairwise_losses_are_elementwise():
     assert loss.reduction == "mean"
     assert torch.allclose(loss.pair_wise(pos, neg), -torch.nn.functional.logsigmoid(pos - neg))
     assert AUCScore(reduction="none")(pos, neg).tolist() == [1, 1, 0]
+
+
+def test_device_pairwise_dataset_csr_and_no_cpu_fallback():
+    """DevicePairWiseDataset's CSRs hold each user's UNIQUE items, sorted
+    (frozenset semantics of base_datasets.py:74-85); sampling itself is HIP
+    only, so a CPU-resident dataset fails loudly instead of falling back."""
+    from divrec.datasets import DevicePairWiseDataset
+    inter = torch.tensor([[0, 5], [0, 2], [0, 5], [2, 7], [2, 1], [2, 9]])
+    fz = torch.tensor([[1, 3], [2, 0]])
+    data = UserItemInteractionsDataset(inter, number_of_users=3, number_of_items=10)
+    frozen = UserItemInteractionsDataset(fz, number_of_users=3, number_of_items=10)
+    ds = DevicePairWiseDataset(data, frozen=frozen, max_sampled=4, device="cpu")
+    rowptr, items = ds.pos_csr
+    assert rowptr.tolist() == [0, 2, 2, 5] and items.tolist() == [2, 5, 1, 7, 9]
+    assert items.dtype == torch.int32 and rowptr.dtype == torch.int64
+    erow, eitems = ds.excl_csr
+    assert erow.tolist() == [0, 0, 1, 2] and eitems.tolist() == [3, 0]
+    assert len(ds) == 3 * 16
+    with pytest.raises(RuntimeError):
+        next(iter(ds.loader(batch_size=8)))
+    with pytest.raises(ValueError):
+        DevicePairWiseDataset(data, max_sampled=0, device="cpu")
