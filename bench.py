@@ -477,13 +477,26 @@ def secondary(args):
             t = time.perf_counter() - t0
             cpu = {"value": m / t, "unit": "pairs/s", "cores": 1, "kind": "port",
                    "sample": f"oracle.mf_forward (numpy gather + fp32 row sum), {m} pairs, {t:.2f}s"}
+        # the autograd backward of MatrixFactorization.forward (dense embedding
+        # gradients): two row gathers + two rows of fp32 atomic adds per pair
+        gU, gI = torch.zeros_like(Ut), torch.zeros_like(It)
+        gout = torch.randn(n, generator=g, device=dev)
+        bwall, bdt = _timed(lambda: ops.gather_dot_backward(Ut, It, uid, iid, gout, gU, gI),
+                            args.steps, args.warmup)
+        added = 2 * d * 4 * n
+        backward = {"value": n / bwall, "unit": "pairs/s", "ms": bdt * 1e3,
+                    "kernel": "dr_gather_dot_backward",
+                    "hbm_roofline": _hbm((2 * d * 4 + 2 * 8 + 4) * n + added, bdt),
+                    "atomic_roofline": {"bound": "fp32 atomics", "added_bytes": added,
+                                        "achieved": added / bdt / 1e9, "peak": ATOMIC_F32_GBS,
+                                        "unit": "GB/s", "frac": added / bdt / 1e9 / ATOMIC_F32_GBS}}
         _line("MatrixFactorization.forward gathered pairs/sec (fp32 1M x 1M d=128)", n / wall,
               "pairs/s", args, wall, "f32",
               {"workload": f"dr_gather_dot, {n} uniform random (user, item) pairs, fp32 tables "
                            f"{U_n}x{d} and {I_n}x{d}", "pairs": n, "dim": d},
               dict(_hbm(per_pair * n, dt), kernel="dr_gather_dot",
                    per_unit=f"{per_pair} B/pair = 2 rows x {d} x 4 B + 2 ids x 8 B + 4 B out"),
-              cpu)
+              cpu, backward=backward)
         return 0
 
     if args.workload == "bpr":

@@ -37,6 +37,10 @@ struct Vec16<__bf16> {
   }
 };
 
+#ifndef DR_BWD_ROWS
+#define DR_BWD_ROWS 1  // backward: contiguous 32-lane row layout (0: 16-B chunks per lane)
+#endif
+
 constexpr int kUnroll = 4;
 constexpr int kBlock = 256;
 
@@ -133,6 +137,43 @@ __global__ __launch_bounds__(kBlock) void gather_dot_bwd_vec(
   }
 }
 
+// Backward with the BPR kernel's contiguous row layout: a group of 32 lanes
+// owns a pair and lane l handles elements l, l+32, ..., so every load and
+// every atomic wave-instruction covers two contiguous 128-B row segments (the
+// shape at which global_atomic_add_f32 runs at full rate; the 16-B-per-lane
+// chunks of gather_dot_bwd_vec scatter each atomic instruction over 16-B
+// strides). EPL = elements per lane = ceil(d / 32), any d <= 512.
+template <int EPL>
+__global__ __launch_bounds__(kBlock) void gather_dot_bwd_rows(
+    const float* __restrict__ U, const float* __restrict__ I, int64_t d,
+    const int64_t* __restrict__ uid, const int64_t* __restrict__ iid, int64_t n,
+    const float* __restrict__ gout, float* __restrict__ gU, float* __restrict__ gI) {
+  const int gl = threadIdx.x & 31;
+  const int64_t group = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 5;
+  const int64_t ngroups = (int64_t)gridDim.x * (kBlock / 32);
+  for (int64_t p = group; p < n; p += ngroups) {
+    const int64_t u = uid[p], i = iid[p];
+    const float g = gout[p];
+    const float* ur = U + u * d;
+    const float* ir = I + i * d;
+    float uv[EPL], iv[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      const int64_t c = gl + 32 * e;
+      uv[e] = c < d ? ur[c] : 0.f;
+      iv[e] = c < d ? ir[c] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      const int64_t c = gl + 32 * e;
+      if (c < d) {
+        if (gU) atomicAdd(gU + u * d + c, g * iv[e]);
+        if (gI) atomicAdd(gI + i * d + c, g * uv[e]);
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void gather_dot_bwd_generic(
     const float* __restrict__ U, const float* __restrict__ I, int64_t d,
     const int64_t* __restrict__ uid, const int64_t* __restrict__ iid, int64_t n,
@@ -215,6 +256,27 @@ extern "C" int dr_gather_dot_backward(const float* user_table, const float* item
   if (n == 0 || (!grad_user && !grad_item)) return DR_OK;
   DR_CHECK_ARG(user_table && item_table && user_id && item_id && grad_out, "null pointer");
   hipStream_t s = (hipStream_t)stream;
+#if DR_BWD_ROWS
+  if (d <= 512) {
+    const int grid = grid_for(n, kBlock / 32);
+#define DR_BWD(EE)                                                                         \
+  hipLaunchKernelGGL(gather_dot_bwd_rows<EE>, dim3(grid), dim3(kBlock), 0, s, user_table,  \
+                     item_table, d, user_id, item_id, n, grad_out, grad_user, grad_item)
+    switch ((int)dr::ceil_div(d, 32)) {
+      case 1: DR_BWD(1); break;
+      case 2: DR_BWD(2); break;
+      case 3: DR_BWD(3); break;
+      case 4: DR_BWD(4); break;
+      case 5: case 6: DR_BWD(6); break;
+      case 7: case 8: DR_BWD(8); break;
+      case 9: case 10: case 11: case 12: DR_BWD(12); break;
+      default: DR_BWD(16); break;
+    }
+#undef DR_BWD
+    DR_CHECK_LAUNCH();
+    return DR_OK;
+  }
+#endif
   const int64_t chunks = d % 4 == 0 ? d / 4 : -1;
   auto go = [&](auto kern, int G) {
     const int grid = grid_for(n, kBlock / G);

@@ -57,9 +57,9 @@ def test_gather_dot_integer_exact():
     assert np.array_equal(got.cpu().numpy(), oracle.mf_forward(U, I, uid, iid))
 
 
-def test_gather_dot_backward():
-    rng = np.random.default_rng(3)
-    d = 64
+@pytest.mark.parametrize("d", [32, 64, 100, 128, 300])
+def test_gather_dot_backward(d):
+    rng = np.random.default_rng(3 + d)
     U = rng.standard_normal((40, d)).astype(np.float32)
     I = rng.standard_normal((60, d)).astype(np.float32)
     uid, iid = rng.integers(0, 40, 2000), rng.integers(0, 60, 2000)
