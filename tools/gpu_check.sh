@@ -1,0 +1,6 @@
+#!/bin/bash
+# Full parity suite + smoke on the committed tree.
+set -e
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/c_tests.log 2>&1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/c_smoke.log 2>&1
