@@ -1,0 +1,897 @@
+// The streaming score scan of dr_score_topk (csrc/score_topk.hip), shared by
+// the per-dtype translation units score_scan_bf16.hip and score_scan_f32.hip.
+//
+// score_scan_kernel<W, CAP, SEEDED, F32> — one 512-thread workgroup (8 waves,
+//   two per SIMD) owns UPWG = 8*NU_T*32 users and streams one chunk of the item
+//   catalog, so every item byte staged in LDS feeds UPWG products.
+//   * W is the row width in bf16 units (row bytes / 2): a bf16 table of width d
+//     has W = d, an fp32 table W = 2d. Geometry (stages, user tiles, LDS
+//     swizzle, 16-B fragments) depends only on the row bytes, so both dtypes
+//     share it; only the MFMA differs (kstep_mma).
+//   * Each wave keeps the rows of its NU_T*32 users resident in registers as
+//     MFMA B fragments for the whole scan.
+//   * Item rows go HBM -> LDS by LDS-DMA (global_load_lds_dwordx4) into a ring
+//     of stages (W = 128: two 64-KB slots, one stage ahead; else three
+//     32-KB slots, two ahead), one s_barrier per stage; the LDS image is
+//     XOR-swizzled through the per-lane source address so the A-fragment
+//     ds_read_b128s are bank-conflict-free. All 8 waves share every stage.
+//     A fragments are read two k-steps ahead of the MFMAs that use them.
+//   * The 32x32 MFMAs put items on M and users on N, so a lane holds 16 scores
+//     of ONE user: the hot epilogue is a 16-way max and one compare with that
+//     user's running threshold. Scores never leave registers. The two waves of
+//     a SIMD cover each other's epilogues.
+//   * Survivors are stored straight into per-user candidate buffers in HBM
+//     (slot from a per-user LDS counter), or for W <= 64 staged in LDS and
+//     resolved per stage. Once a buffer holds more than k + kSlack + kFlushGap
+//     keys the wave compacts it with an in-register radix select, keeping only
+//     keys that can still reach the top k, and raises the user's threshold to
+//     the selected bound.
+//   * Guessed thresholds (SEEDED = true): a scan of a strided sample sets each
+//     user's starting threshold; users the guess failed are rescanned.
+//   * All VMEM traffic inside the scan (LDS-DMA and candidate stores) is
+//     issued from inline asm and counted by the wave, so each stage wait is an
+//     exact s_waitcnt vmcnt(N): no drain of the ring.
+#pragma once
+
+#include "common.h"
+
+namespace dr_topk {
+
+
+using dr::bf16x8;
+using dr::f32x16;
+
+// Diagnostic build (-DDR_TOPK_DIAG, libdivrec_hip_diag.so only): per-wave
+// s_memtime cycle counters of each phase of the scan, written to the tail of
+// the workspace. Never compiled into the product library.
+#ifdef DR_TOPK_DIAG
+#define DG_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define DG_ADD(slot, t0) dg[slot] += __builtin_amdgcn_s_memtime() - (t0)
+#define DG_CNT(slot) dg[slot] += 1
+#else
+#define DG_T0(v) ((void)0)
+#define DG_ADD(slot, t0) ((void)0)
+#define DG_CNT(slot) ((void)0)
+#endif
+enum {
+  kDgTotal, kDgPrologue, kDgBoundary, kDgMma, kDgHits, kDgEnqueue, kDgDrain, kDgFlush,
+  kDgNTiles, kDgNEnqueue, kDgNDrain, kDgNFlush, kDgNStages, kDgRealtime, kDgSlots = 16
+};
+
+// Geometry knobs. The defaults are the product configuration; the -D
+// overrides exist so tools/variant_bench.py can time alternatives side by side
+// (build_native.py --variant NAME -D KEY=VAL).
+#ifndef DR_STAGE_BYTES
+#define DR_STAGE_BYTES 32768  // one LDS ring slot, d != 128
+#endif
+#ifndef DR_RING
+#define DR_RING 3  // ring slots (RING - 1 stages in flight), d != 128
+#endif
+#ifndef DR_STAGE_BYTES_WIDE
+#define DR_STAGE_BYTES_WIDE 65536  // ring slot for d = 128
+#endif
+#ifndef DR_RING_WIDE
+#define DR_RING_WIDE 2  // ring slots for d = 128
+#endif
+#ifndef DR_NUT
+#define DR_NUT 4  // user tiles of 32 per wave for d = 128
+#endif
+#ifndef DR_NUT_NARROW
+#define DR_NUT_NARROW 8  // user tiles of 32 per wave for d <= 64 (measured: 8 is +14 % at d=64, 1M x 1M)
+#endif
+#ifndef DR_PRIO
+#define DR_PRIO 0  // static s_setprio 1 for waves 4-7 (measured: no gain)
+#endif
+#ifndef DR_APIPE
+#define DR_APIPE 1  // A fragments read two k-steps ahead
+#endif
+#ifndef DR_FLUSH_GAP
+#define DR_FLUSH_GAP 96  // new keys a buffer takes past k + kSlack before compaction
+#endif
+#ifndef DR_ENQ_STAGED
+// survivors: 0 = direct per-lane enqueue, 1 = stage lane blocks in LDS and
+// resolve them per stage, 2 = staged for d <= 64 only (measured: staged is 4%
+// faster at d=64, where survivors per MFMA are twice as dense, and 4% slower
+// at d=128)
+#define DR_ENQ_STAGED 2
+#endif
+#ifndef DR_ENQ_FAST
+#define DR_ENQ_FAST 1  // direct enqueue: one-survivor lanes store their max (no value select)
+#endif
+#ifndef DR_STAGE_BLOCKS
+#define DR_STAGE_BLOCKS 64  // staged lane blocks per wave (>= 64: one user tile always fits)
+#endif
+#ifndef DR_COMPACT_INLINE
+#define DR_COMPACT_INLINE __noinline__
+#endif
+
+constexpr int kWaves = 8;  // two waves per SIMD: 256-register budget each
+constexpr int kThreads = kWaves * 64;
+constexpr int kTileItems = 32;
+#ifndef DR_SLACK
+#define DR_SLACK 32
+#endif
+constexpr int kSlack = DR_SLACK;  // keys kept beyond k by a compaction
+constexpr int kFlushGap = DR_FLUSH_GAP;
+
+// Stage geometry per row width. d = 128: two 64-KB slots (one barrier per
+// 8 tiles at d=128; measured against three 32-KB slots: +2 % at 10M items,
+// +6 % at 1.25M, where the survivor stream makes per-stage wave imbalance
+// larger). d <= 64: three 32-KB slots (its LDS survivor staging needs room;
+// 64-KB stages measured -10 % there; d = 256 spills with them).
+constexpr int stage_bytes_for(int w) { return w == 128 ? DR_STAGE_BYTES_WIDE : DR_STAGE_BYTES; }
+constexpr int ring_for(int w) { return w == 128 ? DR_RING_WIDE : DR_RING; }
+
+template <int D>  // D = W, the row's width in bf16 units (row bytes / 2)
+struct TileGeom {
+  static constexpr int STAGE_BYTES = stage_bytes_for(D);  // one LDS ring slot
+  static constexpr int RING = ring_for(D);                // slots (RING - 1 stages in flight)
+  static constexpr int LPT = STAGE_BYTES / 16 / kThreads;  // LDS-DMA per thread per stage
+  static constexpr int KSTEPS = D / 16;                 // MFMA k-steps per row
+  static constexpr int CPR = D / 8;                     // 16-B chunks per row
+  static constexpr int TILE_BYTES = kTileItems * D * 2;
+  static constexpr int SR = STAGE_BYTES / TILE_BYTES;   // row tiles per stage
+  static_assert(LPT >= 1 && STAGE_BYTES % (16 * kThreads) == 0, "stage geometry");
+  static_assert(RING >= 2, "ring depth");
+  static constexpr int RPB = (2 * D >= 256) ? 1 : 256 / (2 * D);  // rows per 256-B bank row
+  static constexpr int SWM = (CPR < 16 ? CPR : 16) - 1;
+  static constexpr int MARGIN = SR * kTileItems;  // max new keys per user per stage
+  static_assert(SR >= 1, "a stage holds at least one tile");
+  // physical chunk = logical chunk ^ swz(row): spreads the 32 rows that one
+  // A-fragment ds_read_b128 touches over distinct 16-B bank slots.
+  __device__ static int swz(int r) { return (r / RPB) & SWM; }
+};
+
+// User tiles (of 32) per wave. The B fragments take NU_T*KSTEPS*4 VGPRs (128 at
+// d=128, NU_T=4; 128 at d=64, NU_T=8). The tiles are scored in groups of at
+// most four against each item tile, one accumulator set (4*16 VGPRs) reused
+// by the groups, so narrow rows can hold more users per wave.
+constexpr int nut_for(int w) {
+  return w >= 512 ? 1 : (w >= 256 ? 2 : (w <= 64 ? DR_NUT_NARROW : DR_NUT));
+}
+constexpr int ngroup_for(int w) { return nut_for(w) > 4 ? 4 : nut_for(w); }
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ asm VMEM
+// The scan issues its VMEM traffic from inline asm so that hipcc does not put
+// its own conservative s_waitcnt vmcnt(0) in front of the MFMAs (it cannot
+// prove a C++ ds_read does not alias an in-flight LDS-DMA); the wave counts
+// every instruction it issues and waits with exact counts. M0 is used by no
+// other code in the kernel.
+__device__ __forceinline__ void st64(uint64_t* p, uint64_t v) {
+  asm volatile("global_store_dwordx2 %0, %1, off" : : "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ u32x4 ds_read_b128_asm(uint32_t lds_addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr));
+  return v;
+}
+// LDS waits that name the fragment they retire ("+v"): no consumer of it can
+// be scheduled above the wait. lgkmcnt(1) = every LDS read but the youngest
+// has returned (LDS reads return in order; extra younger reads only make the
+// wait stricter).
+__device__ __forceinline__ void lds_wait1(u32x4& v) {
+  asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(v) : : "memory");
+}
+__device__ __forceinline__ void lds_wait0(u32x4& v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v) : : "memory");
+}
+
+// s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at their maxima).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+// Wait until at most n (wave-uniform) VMEM ops are outstanding, rounding n
+// down to a power of two (waits for a little more than required, always
+// correct): six scalar compares instead of a 64-step ladder at every stage.
+__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
+  if (n >= 32) wait_vmcnt<32>();
+  else if (n >= 16) wait_vmcnt<16>();
+  else if (n >= 8) wait_vmcnt<8>();
+  else if (n >= 4) wait_vmcnt<4>();
+  else if (n >= 2) wait_vmcnt<2>();
+  else if (n >= 1) wait_vmcnt<1>();
+  else wait_vmcnt<0>();
+}
+
+// Issue the LDS-DMA of one stage: rows [row0, row0 + SR*32) of the slice into
+// the ring slot at LDS byte address `lds_stage`. The image is lane-linear
+// (glds writes base + lane*16); the swizzle is on the SOURCE address
+// (cdna_hip_programming.md §5.4 rule 21). Rows past the slice end are
+// clamped to its last row; their scores are masked in the epilogue.
+// Addressing is SGPR base (the stage's first row) + a 32-bit per-lane offset
+// recomputed at every stage from the thread id: the empty asm makes the id
+// opaque, so hipcc cannot hoist 64-bit per-lane addresses out of the tile loop
+// (they cost registers the loop does not have, and their spill reloads wait
+// vmcnt(0), draining the ring).
+template <int D>
+__device__ __forceinline__ void issue_stage(const char* __restrict__ I, int64_t n_items,
+                                            int64_t row0, uint32_t lds_stage) {
+  using G = TileGeom<D>;
+  constexpr int ROWS = G::SR * kTileItems;
+  uint32_t tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = (int)(tid & 63u);
+  const int wave = (int)(__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
+  const char* base = I + row0 * (2 * D);
+  const int64_t left = n_items - 1 - row0;
+  const int rmax = left < ROWS - 1 ? (int)left : ROWS - 1;
+#pragma unroll
+  for (int j = 0; j < G::LPT; ++j) {
+    const int wave_first = j * kThreads + wave * 64;  // wave-uniform chunk index
+    const int idx = wave_first + lane;
+    const int r = idx / G::CPR;
+    const int lc = (idx % G::CPR) ^ G::swz(r & 31);
+    const int rr = r < rmax ? r : rmax;
+    const uint32_t off = (uint32_t)(rr * (2 * D) + lc * 16);
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_stage + wave_first * 16);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :
+                 : "v"(off), "s"(base), "s"(m0)
+                 : "memory", "m0");
+#pragma clang diagnostic pop
+  }
+}
+
+__device__ __forceinline__ bool sorted_contains(const int32_t* __restrict__ list, int n,
+                                                int32_t item) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (list[mid] < item) lo = mid + 1; else hi = mid;
+  }
+  return lo < n && list[lo] == item;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lane_prefix(uint64_t bal) {  // set bits of bal below this lane
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+}
+
+struct CompactResult {
+  int kept;
+  float thr;
+};
+
+// Compaction of one candidate buffer (cold path, out of line so its registers
+// do not raise the pressure of the MFMA loop). Keeps only the keys that can
+// still be in the top k: radix select (8 bits per level, wave-wide LDS
+// histogram) down to the bucket holding the k-th largest key, until at most
+// k + kSlack keys remain at or above the bucket's lower bound. The bound's
+// score is the new threshold: >= k kept keys rank above any later item of
+// equal or lower score. Excluded items are dropped first.
+template <int P>
+__device__ DR_COMPACT_INLINE CompactResult compact_buffer(uint64_t* __restrict__ buf, int n_in, int k,
+                                                     const int32_t* __restrict__ ex, int exn,
+                                                     uint32_t* __restrict__ hist) {
+  const int lane = dr::lane_id();
+  wait_vmcnt<0>();  // this wave's candidate stores have landed
+  uint64_t key[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const int e = lane * P + i;
+    key[i] = e < n_in ? __hip_atomic_load(buf + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : 0ull;
+  }
+  if (exn > 0) {
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+      if (key[i] != 0ull && sorted_contains(ex, exn, (int32_t)dr::key_item(key[i])))
+        key[i] = 0ull;
+  }
+  int total = 0;
+#pragma unroll
+  for (int i = 0; i < P; ++i) total += __popcll(__ballot(key[i] != 0ull));
+  uint64_t lo = 1ull;  // keep keys >= lo (key 0 = empty slot)
+  CompactResult res{total, -INFINITY};
+  if (total > k + kSlack) {
+    uint64_t pfx = 0ull;
+    int need = k, above = 0, inb = total;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hist[lane * 4 + j] = 0u;
+      wave_lds_sync();
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const bool in = key[i] != 0ull &&
+                        (shift == 56 || (key[i] >> (shift + 8)) == (pfx >> (shift + 8)));
+        if (in) atomicAdd(&hist[(uint32_t)(key[i] >> shift) & 255u], 1u);
+      }
+      wave_lds_sync();
+      uint32_t hv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hv[j] = hist[lane * 4 + j];
+      const uint32_t s4 = hv[0] + hv[1] + hv[2] + hv[3];
+      uint32_t sfx = s4;  // inclusive suffix sum over lanes >= this lane
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) {
+        const uint32_t o = __shfl_down(sfx, m);
+        sfx += (lane + m < 64) ? o : 0u;
+      }
+      // this lane's bins from the top (4l+3 .. 4l): the one holding rank `need`
+      uint32_t cum = sfx - s4;  // keys in bins above 4l+3
+      int fb = -1;
+      uint32_t fexcl = 0, fcnt = 0;
+#pragma unroll
+      for (int j = 3; j >= 0; --j) {
+        const uint32_t nx = cum + hv[j];
+        if (fb < 0 && cum < (uint32_t)need && (uint32_t)need <= nx) {
+          fb = lane * 4 + j;
+          fexcl = cum;
+          fcnt = hv[j];
+        }
+        cum = nx;
+      }
+      const int src = __builtin_ctzll(__ballot(fb >= 0));
+      const int b = __builtin_amdgcn_readlane(fb, src);
+      const int excl = __builtin_amdgcn_readlane((int)fexcl, src);
+      inb = __builtin_amdgcn_readlane((int)fcnt, src);
+      pfx |= (uint64_t)b << shift;
+      need -= excl;
+      above += excl;
+      wave_lds_sync();  // hist is re-zeroed by the next level
+      if (above + inb <= k + kSlack) break;
+    }
+    lo = pfx;
+    res.kept = above + inb;
+    res.thr = dr::key_score(pfx);                // smallest score with the kept prefix
+    if (res.thr != res.thr) res.thr = -INFINITY;  // prefix below -FLT_MAX decodes to NaN
+  }
+  // write the kept keys back densely (order is irrelevant)
+  int base = 0;
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const bool keep = key[i] >= lo;  // lo >= 1 also drops empty keys
+    const uint64_t bal = __ballot(keep);
+    if (keep) buf[base + lane_prefix(bal)] = key[i];
+    base += __popcll(bal);
+  }
+  wait_vmcnt<0>();
+  return res;
+}
+
+// One k-step (one 16-B A fragment per lane) against NG user tiles.
+//   bf16: one v_mfma_f32_32x32x16_bf16 per tile (lane (col, h) holds row col,
+//         k = 16s + 8h .. +7).
+//   fp32: the same 16 B are four floats k = 8s + 4h + j, j = 0..3; four
+//         v_mfma_f32_32x32x2_f32 per tile, MFMA j summing k = 8s + j and
+//         8s + 4 + j over the two lane halves. The user fragment holds the
+//         same k, so every product of the row pair is taken once. The result
+//         is an exact fp32 fmaf chain (cdna_hip_programming.md, FP32-input MFMA).
+template <bool F32, int NG, int NB, int KS>
+__device__ __forceinline__ void kstep_mma(const u32x4& a, const u32x4 (&bfr)[NB][KS], int g0, int s,
+                                          f32x16 (&acc)[NG]) {
+  if constexpr (F32) {
+    const dr::f32x4 av = __builtin_bit_cast(dr::f32x4, a);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ut = 0; ut < NG; ++ut) {
+        const dr::f32x4 bv = __builtin_bit_cast(dr::f32x4, bfr[g0 + ut][s]);
+        acc[ut] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc[ut], 0, 0, 0);
+      }
+  } else {
+#pragma unroll
+    for (int ut = 0; ut < NG; ++ut)
+      acc[ut] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                        __builtin_bit_cast(bf16x8, bfr[g0 + ut][s]),
+                                                        acc[ut], 0, 0, 0);
+  }
+}
+
+struct TopkArgs {
+  const char* U;  // user table rows: W * 2 bytes each
+  const int64_t* user_ids;
+  int64_t n_users;
+  int64_t n_users_pad;  // n_ublocks * UPWG: candidate buffers exist for padded users too
+  const char* I;  // item slice rows: W * 2 bytes each
+  int64_t n_items;
+  int64_t item_base;
+  int k;
+  const int64_t* excl_rowptr;
+  const int32_t* excl_items;
+  int n_chunks;
+  int64_t chunk_items;  // multiple of the stage's item count
+  int64_t n_ublocks;
+  const float* init_thr;  // [n_users_pad] starting thresholds (SEEDED scans only)
+  // Fallback rescan only: the user count lives on the device (n_users and
+  // n_ublocks above are its upper bounds), and pos_map[p] is the caller's
+  // position of list entry p (its exclusion row). NULL otherwise.
+  const int32_t* n_users_dev;
+  const int64_t* pos_map;
+  uint64_t* cand;  // [n_chunks][n_users_pad][CAP] keys (unsorted)
+  int32_t* cnt;    // [n_chunks][n_users_pad] valid keys per buffer
+  uint64_t* diag;  // [gridDim.x * kWaves][kDgSlots] in DR_TOPK_DIAG builds
+};
+
+template <int W, int CAP, bool SEEDED, bool F32>
+__global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
+  constexpr int D = W;  // geometry is by row bytes: an fp32 row of d is a bf16 row of 2d
+  using G = TileGeom<D>;
+  constexpr int NU_T = nut_for(D);
+  constexpr int NG = ngroup_for(D);  // user tiles per accumulator group
+  constexpr int NGRP = NU_T / NG;    // groups scored against each item tile
+  static_assert(NGRP * NG == NU_T && NGRP <= 2, "user tile groups");
+  constexpr int KS = G::KSTEPS;
+  constexpr int SR = G::SR;
+  constexpr int UPW = NU_T * 32;      // users per wave
+  constexpr int UPWG = UPW * kWaves;  // users per workgroup
+  constexpr int P = CAP / 64;         // keys per lane in a compaction
+  constexpr int kRing = G::RING;
+  constexpr int kStageBytes = G::STAGE_BYTES;
+  constexpr int kLpt = G::LPT;
+  constexpr int RING_BYTES = kRing * kStageBytes;
+  // per wave: per-user key counts, radix histogram, staged survivor blocks
+  // (16 scores + item base + slot + threshold each)
+  constexpr bool STAGED = DR_ENQ_STAGED == 1 || (DR_ENQ_STAGED == 2 && D <= 64);
+  constexpr int SB = STAGED ? DR_STAGE_BLOCKS : 0;
+  // stage_hits resolves a full stage area, then stages up to 64 lanes of one
+  // user tile: the area must hold a whole wave's worth of blocks
+  static_assert(!STAGED || SB >= 64, "staging area smaller than a wave");
+  constexpr int WAVE_BYTES = UPW * 4 + 256 * 4 + SB * (64 + 12);
+  static_assert(RING_BYTES + kWaves * WAVE_BYTES <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[RING_BYTES + kWaves * WAVE_BYTES];
+
+  // A buffer is compacted once it holds more than flush_at keys; a stage adds
+  // at most MARGIN keys per user, so flush_at + MARGIN <= CAP. A small gap
+  // above k + kSlack keeps the thresholds close to the running k-th score.
+  // Unseeded scans start at -inf: every score of the first stages is a
+  // survivor until the first compaction sets a real threshold.
+  int flush_at = a.k + kSlack + kFlushGap;
+  flush_at = flush_at < CAP - G::MARGIN ? flush_at : CAP - G::MARGIN;
+
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  const int col = lane & 31;
+#if DR_PRIO
+  // The second-dispatched half of the workgroup loses VALU arbitration to its
+  // SIMD partner on every segment; one static priority bump evens the pair
+  // (cdna_hip_programming.md T5, static form). Wave-uniform by readfirstlane.
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
+  char* wbase = smem + RING_BYTES + wave * WAVE_BYTES;
+  uint32_t* ucnt = reinterpret_cast<uint32_t*>(wbase);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(wbase + UPW * 4);
+  float* blk_val = reinterpret_cast<float*>(wbase + UPW * 4 + 1024);  // [SB][16], 16-B aligned
+  uint32_t* blk_gbase = reinterpret_cast<uint32_t*>(blk_val + SB * 16);
+  uint32_t* blk_slot = blk_gbase + SB;  // slot | h << 16 | valid rows << 17
+  float* blk_thr = reinterpret_cast<float*>(blk_slot + SB);
+  const uint32_t lds_ring = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  // This lane's A-fragment byte offset for k-step s in a tile is
+  // col*2D + ((2s + h) ^ swz(col)) * 16 = a_row + ((2s) ^ a_sw) * 16: two VALU
+  // per read instead of KS resident offsets (registers are the budget here).
+  const uint32_t a_row = (uint32_t)(col * (2 * D));
+  const uint32_t a_sw = (uint32_t)(h ^ G::swz(col));
+  auto a_off = [&](int s) -> uint32_t { return a_row + ((((uint32_t)(2 * s)) ^ a_sw) << 4); };
+
+#ifdef DR_TOPK_DIAG
+  uint64_t dg[kDgSlots] = {};
+  DG_T0(t_kernel);
+  const uint64_t rt_kernel = __builtin_amdgcn_s_memrealtime();  // 100 MHz: clock = cycles / time
+#endif
+  int64_t n_users = a.n_users, n_ublocks = a.n_ublocks;
+  if (a.n_users_dev) {  // fallback rescan: only the users the guess failed
+    const int64_t n = __builtin_amdgcn_readfirstlane(*a.n_users_dev);
+    n_users = n < n_users ? n : n_users;
+    n_ublocks = (n_users + UPWG - 1) / UPWG;
+  }
+  const int64_t n_units = n_ublocks * a.n_chunks;
+  for (int64_t unit = blockIdx.x; unit < n_units; unit += gridDim.x) {
+    DG_T0(t_pro);
+    const int64_t chunk = unit / n_ublocks;
+    const int64_t ub = unit % n_ublocks;
+    const int64_t i_beg = chunk * a.chunk_items;
+    int64_t i_end = i_beg + a.chunk_items;
+    i_end = i_end < a.n_items ? i_end : a.n_items;
+    const int ntiles = i_end > i_beg ? (int)((i_end - i_beg + kTileItems - 1) / kTileItems) : 0;
+    const int nst = (ntiles + SR - 1) / SR;
+    const int64_t upos0 = ub * UPWG + (int64_t)wave * UPW;  // first user position of the wave
+    uint64_t* cbase = a.cand + ((size_t)chunk * a.n_users_pad + upos0) * CAP;
+
+    // Resident B fragments: lane holds user (ut*32+col), k = 16s + 8h .. +7.
+    u32x4 bfr[NU_T][KS];  // bf16x8 (bf16 tables) or f32x4 (fp32 tables) per k-step
+    float thr[NU_T];
+#pragma unroll
+    for (int ut = 0; ut < NU_T; ++ut) {
+      const int64_t pos = upos0 + ut * 32 + col;
+      int64_t row = 0;
+      if (pos < n_users) row = a.user_ids ? a.user_ids[pos] : pos;
+      const uint4* src = reinterpret_cast<const uint4*>(a.U + row * (2 * D) + 16 * h);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) bfr[ut][s] = __builtin_bit_cast(u32x4, src[2 * s]);
+      thr[ut] = SEEDED ? a.init_thr[pos] : -INFINITY;
+    }
+    // Retire those loads where the compiler can see it (else it waits for them
+    // inside the loop, draining the ring).
+    wait_vmcnt<0>();
+    for (int s = lane; s < UPW; s += 64) ucnt[s] = 0;
+    int vmc = 0;        // VMEM instructions issued by this wave in this unit
+    int vm_done = 0;    // every op issued before this count has completed
+    int vs[kRing - 1];  // vmc right after each outstanding stage's DMA
+#pragma unroll
+    for (int i = 0; i < kRing - 1; ++i) vs[i] = 0;
+    DG_ADD(kDgPrologue, t_pro);
+
+    // -------------------------------------------------------------- MFMA tile
+    auto mma_tile = [&](int t, f32x16 (&acc)[NG], auto GI) {
+      constexpr int g0 = decltype(GI)::value * NG;
+      const uint32_t tb = lds_ring + ((t / SR) % kRing) * kStageBytes + (t % SR) * G::TILE_BYTES;
+#pragma unroll
+      for (int ut = 0; ut < NG; ++ut) acc[ut] = f32x16{};
+#if DR_APIPE
+      // Fragment s is read two k-steps before its MFMAs; each wait retires
+      // exactly the fragment the next MFMAs consume.
+      u32x4 af[KS];
+      af[0] = ds_read_b128_asm(tb + a_off(0));
+      if constexpr (KS > 1) af[1] = ds_read_b128_asm(tb + a_off(1));
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        if (s + 1 < KS) lds_wait1(af[s]);
+        else lds_wait0(af[s]);
+        if (s + 2 < KS) af[s + 2] = ds_read_b128_asm(tb + a_off(s + 2));
+        kstep_mma<F32, NG>(af[s], bfr, g0, s, acc);
+      }
+#else
+      constexpr int HALF = KS >= 4 ? KS / 2 : KS;
+#pragma unroll
+      for (int s0 = 0; s0 < KS; s0 += HALF) {
+        u32x4 af[HALF];
+#pragma unroll
+        for (int s = 0; s < HALF; ++s) af[s] = ds_read_b128_asm(tb + a_off(s0 + s));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < HALF; ++s) kstep_mma<F32, NG>(af[s], bfr, g0, s0 + s, acc);
+      }
+#endif
+    };
+
+    // -------------------------------------------------------------- cold paths
+    auto compact = [&](int ut, int c, int n_in) {
+      DG_T0(t_f);
+      const int slot = ut * 32 + c;
+      const int64_t upos = upos0 + slot;
+      const int32_t* ex = nullptr;
+      int exn = 0;
+      if (a.excl_rowptr && upos < n_users) {
+        const int64_t er = a.pos_map ? a.pos_map[upos] : upos;
+        const int64_t e0 = a.excl_rowptr[er], e1 = a.excl_rowptr[er + 1];
+        ex = a.excl_items + e0;
+        exn = (int)(e1 - e0);
+      }
+      const CompactResult r = compact_buffer<P>(cbase + (size_t)slot * CAP, n_in, a.k, ex, exn, hist);
+      vm_done = vmc;
+      if (lane == 0) ucnt[slot] = (uint32_t)r.kept;
+      wave_lds_sync();
+#pragma unroll
+      for (int u2 = 0; u2 < NU_T; ++u2)
+        if (u2 == ut && col == c) thr[u2] = fmaxf(thr[u2], r.thr);  // both bounds are valid
+      DG_ADD(kDgFlush, t_f);
+      DG_CNT(kDgNFlush);
+    };
+
+    auto check_compact = [&]() {
+#pragma unroll
+      for (int ut = 0; ut < NU_T; ++ut) {
+        const uint32_t c_cnt = ucnt[ut * 32 + col];
+        uint64_t need = __ballot(c_cnt > (uint32_t)flush_at) & 0xffffffffull;
+        while (need) {
+          const int c = __builtin_ctzll(need);
+          need &= need - 1;
+          compact(ut, c, __builtin_amdgcn_readlane((int)c_cnt, c));
+        }
+      }
+    };
+
+    // -------------------------------------------------------------- epilogues
+    // Hot test (branch-free): per user tile, a 16-way max against the threshold.
+    auto any_hits = [&](f32x16 (&acc)[NG], auto GI) -> uint32_t {
+      constexpr int g0 = decltype(GI)::value * NG;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int ut = 0; ut < NG; ++ut) {
+        float m = acc[ut][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) m = fmaxf(m, acc[ut][r]);
+        bits |= (__ballot(m > thr[g0 + ut]) != 0ull ? 1u : 0u) << ut;
+      }
+      return bits;
+    };
+
+    // Append survivors straight to their users' candidate buffers in HBM: one
+    // key per lane per round, its slot from the user's LDS key counter. No
+    // call and no queue in the hot loop, so nothing forces the accumulators
+    // and B fragments out of registers. A stage adds at most MARGIN keys per
+    // user, so a buffer compacted at the stage end never overflows.
+    auto enqueue = [&](int t, f32x16 (&acc)[NG], uint32_t hit_bits, auto GI) {
+      constexpr int g0 = decltype(GI)::value * NG;
+      DG_T0(t_e);
+      const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
+      const int valid = (int)((i_end - tile0) < kTileItems ? (i_end - tile0) : kTileItems);
+      const uint32_t gbase = (uint32_t)(a.item_base + tile0);
+      uint32_t vmask = 0xffffu;  // rows past the slice end (last tile only)
+      if (valid < kTileItems) {
+        vmask = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+          vmask |= (row < valid ? 1u : 0u) << r;
+        }
+      }
+#pragma unroll
+      for (int ut = 0; ut < NG; ++ut) {
+        if (!(hit_bits & (1u << ut))) continue;
+        uint32_t mask = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mask |= (acc[ut][r] > thr[g0 + ut] ? 1u : 0u) << r;
+        mask &= vmask;
+        const int slot = (g0 + ut) * 32 + col;
+        uint64_t* ubuf = cbase + (size_t)slot * CAP;  // this lane's user buffer
+#if DR_ENQ_FAST
+        // Common case: every hitting lane holds ONE survivor. It is then the
+        // lane's maximum (all other scores are <= thr < it), so one round
+        // stores it without the 16-way value select. Full tiles only (the
+        // max of a partial tile may sit in a row past the slice end).
+        if (vmask == 0xffffu && __ballot((mask & (mask - 1u)) != 0u) == 0ull) {
+          if (__ballot(mask != 0u) != 0ull) {
+            float m = acc[ut][0];
+#pragma unroll
+            for (int q = 1; q < 16; ++q) m = fmaxf(m, acc[ut][q]);
+            if (mask != 0u) {
+              const int r = __builtin_ctz(mask);
+              const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+              const uint32_t pos = atomicAdd(&ucnt[slot], 1u);
+              if (pos < (uint32_t)CAP) st64(ubuf + pos, dr::make_key(m, gbase + (uint32_t)row));
+            }
+            vmc += 1;  // the store above issued once (some lane had a key)
+          }
+          continue;
+        }
+#endif
+        while (__ballot(mask != 0u) != 0ull) {
+          const bool has = mask != 0u;
+          const int r = has ? __builtin_ctz(mask) : 0;
+          mask &= mask - 1u;
+          float v = acc[ut][0];
+#pragma unroll
+          for (int q = 1; q < 16; ++q) v = (r == q) ? acc[ut][q] : v;
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (has) {
+            const uint32_t pos = atomicAdd(&ucnt[slot], 1u);
+            if (pos < (uint32_t)CAP)  // always true (flush_at + MARGIN <= CAP): a guard only
+              st64(ubuf + pos, dr::make_key(v, gbase + (uint32_t)row));
+          }
+          vmc += 1;  // the store above issued once (some lane had a key)
+        }
+      }
+      DG_ADD(kDgEnqueue, t_e);
+      DG_CNT(kDgNEnqueue);
+    };
+
+    // -------------------------------------------------------------- tile scan
+    // Stage boundary s: wait (exact count) for this wave's DMA of stage s, a
+    // raw barrier publishes the whole stage, then stage s+kRing-1 is issued
+    // into the slot of stage s-1, which every wave finished reading.
+    auto boundary = [&](int st) {
+      DG_T0(t_b);
+      if (vs[0] > vm_done) wait_vmcnt_dyn(vmc - vs[0]);
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int i = 0; i + 1 < kRing - 1; ++i) vs[i] = vs[i + 1];
+      if (st + kRing - 1 < nst) {
+        issue_stage<D>(a.I, a.n_items, i_beg + (int64_t)(st + kRing - 1) * SR * kTileItems,
+                       lds_ring + ((st + kRing - 1) % kRing) * kStageBytes);
+        vmc += kLpt;
+      }
+      vs[kRing - 2] = vmc;
+      DG_ADD(kDgBoundary, t_b);
+      DG_CNT(kDgNStages);
+    };
+    for (int st = 0; st < kRing - 1 && st < nst; ++st) {
+      issue_stage<D>(a.I, a.n_items, i_beg + (int64_t)st * SR * kTileItems,
+                     lds_ring + st * kStageBytes);
+      vmc += kLpt;
+#pragma unroll
+      for (int i = 0; i < kRing - 1; ++i)
+        if (i == st) vs[i] = vmc;
+    }
+    // Staged survivors. In the tile loop a lane whose 16 scores of a user tile
+    // beat the user's threshold only copies them to an LDS block (four
+    // ds_write_b128 + its item base, slot and threshold); resolve() later
+    // turns the staged blocks into candidate keys with one lane per block, so
+    // the per-score tests, value selects and LDS counter atomics run in
+    // parallel across blocks, off the MFMA loop. A block's threshold is the one
+    // at staging time: thresholds only rise, so it admits a superset.
+    int nblk = 0;  // staged blocks (wave-uniform)
+    auto resolve = [&]() {
+      DG_T0(t_d);
+      wave_lds_sync();
+#pragma unroll 1
+      for (int b0 = 0; b0 < nblk; b0 += 64) {
+        const int i = b0 + lane;
+        const bool live = i < nblk;
+        const int ii = live ? i : 0;
+        const uint32_t gb = blk_gbase[ii];
+        const uint32_t info = blk_slot[ii];  // slot | h << 16 | valid rows << 17
+        const float th = blk_thr[ii];
+        const uint32_t slot = info & 0xffffu;
+        const int hh = (int)((info >> 16) & 1u);
+        const int vld = live ? (int)(info >> 17) : 0;
+        uint64_t* ubuf = cbase + (size_t)slot * CAP;
+        const float4* src = reinterpret_cast<const float4*>(blk_val + ii * 16);
+        // four registers (one float4) at a time: few VGPRs, so this also runs
+        // inside stage_hits with the accumulators live
+#pragma unroll 1
+        for (int q = 0; q < 4; ++q) {
+          const float4 v4 = src[q];
+          const float vq[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = j + 8 * q + 4 * hh;  // score register r = 4q + j
+            const bool hit = row < vld && vq[j] > th;
+            if (__ballot(hit) != 0ull) {
+              if (hit) {
+                const uint32_t pos = atomicAdd(&ucnt[slot], 1u);
+                // pos < CAP always holds (flush_at + MARGIN <= CAP); the test
+                // keeps a broken invariant from ever writing past the buffer
+                if (pos < (uint32_t)CAP) st64(ubuf + pos, dr::make_key(vq[j], gb + (uint32_t)row));
+              }
+              vmc += 1;  // one store instruction (some lane had a key)
+            }
+          }
+        }
+      }
+      nblk = 0;
+      wave_lds_sync();
+      DG_ADD(kDgDrain, t_d);
+      DG_CNT(kDgNDrain);
+    };
+    auto stage_hits = [&](int t, f32x16 (&acc)[NG], uint32_t hit_bits, auto GI) {
+      constexpr int g0 = decltype(GI)::value * NG;
+      DG_T0(t_e);
+      const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
+      const int valid = (int)((i_end - tile0) < kTileItems ? (i_end - tile0) : kTileItems);
+      const uint32_t gbase = (uint32_t)(a.item_base + tile0);
+#pragma unroll
+      for (int ut = 0; ut < NG; ++ut) {
+        if (!(hit_bits & (1u << ut))) continue;
+        float m = acc[ut][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) m = fmaxf(m, acc[ut][r]);
+        const bool hit = m > thr[g0 + ut];
+        const uint64_t bal = __ballot(hit);
+        if (bal == 0ull) continue;
+        const int n = __popcll(bal);
+        if (nblk + n > SB) resolve();  // rare (a scan's first stages): few registers
+        if (hit) {
+          const int i = nblk + lane_prefix(bal);
+          float4* dst = reinterpret_cast<float4*>(blk_val + i * 16);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            dst[q] = make_float4(acc[ut][4 * q], acc[ut][4 * q + 1], acc[ut][4 * q + 2],
+                                 acc[ut][4 * q + 3]);
+          blk_gbase[i] = gbase;
+          blk_slot[i] =
+              (uint32_t)((g0 + ut) * 32 + col) | ((uint32_t)h << 16) | ((uint32_t)valid << 17);
+          blk_thr[i] = thr[g0 + ut];
+        }
+        nblk += n;
+      }
+      DG_ADD(kDgEnqueue, t_e);
+      DG_CNT(kDgNEnqueue);
+    };
+    auto epilogue = [&](int t, f32x16 (&acc)[NG], auto GI) {
+      DG_T0(t_h);
+      uint32_t hit_bits = any_hits(acc, GI);
+      DG_ADD(kDgHits, t_h);
+      hit_bits = __builtin_amdgcn_readfirstlane(hit_bits);  // ballots: uniform
+      // the stage-end work runs after the last group of the tile
+      constexpr bool last_group = decltype(GI)::value == NGRP - 1;
+      if constexpr (STAGED) {
+        if (hit_bits != 0u) stage_hits(t, acc, hit_bits, GI);
+        // end of a stage: resolve the staged blocks, compact full buffers
+        if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) {
+          if (nblk > 0) resolve();
+          check_compact();
+        }
+      } else {
+        if (hit_bits != 0u) enqueue(t, acc, hit_bits, GI);
+        // end of a stage: compact the buffers that passed flush_at
+        if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) check_compact();
+      }
+    };
+    // One accumulator set: the partner wave on the same SIMD issues its MFMAs
+    // while this wave runs the epilogue (two waves per SIMD by design).
+    f32x16 acc[NG];
+    for (int t = 0; t < ntiles; ++t) {
+      DG_CNT(kDgNTiles);
+      if (t % SR == 0) boundary(t / SR);
+      DG_T0(t_m);
+      mma_tile(t, acc, IC<0>{});
+      DG_ADD(kDgMma, t_m);
+      epilogue(t, acc, IC<0>{});
+      if constexpr (NGRP > 1) {
+        DG_T0(t_m2);
+        mma_tile(t, acc, IC<1>{});
+        DG_ADD(kDgMma, t_m2);
+        epilogue(t, acc, IC<1>{});
+      }
+    }
+    wait_vmcnt<0>();
+    wave_lds_sync();
+    for (int s = lane; s < UPW; s += 64)
+      a.cnt[(size_t)chunk * a.n_users_pad + upos0 + s] = (int32_t)ucnt[s];
+    __syncthreads();  // the ring is refilled by the next unit
+  }
+#ifdef DR_TOPK_DIAG
+  DG_ADD(kDgTotal, t_kernel);
+  dg[kDgRealtime] = __builtin_amdgcn_s_memrealtime() - rt_kernel;
+  if (lane == 0 && a.diag) {  // the rescan (usually empty) leaves the main scan's record
+    uint64_t* o = a.diag + ((size_t)blockIdx.x * kWaves + wave) * kDgSlots;
+#pragma unroll
+    for (int i = 0; i < kDgSlots; ++i) o[i] = dg[i];
+  }
+#endif
+}
+
+// ------------------------------------------------------------------ launch plan
+struct Plan {
+  int cap;
+  int users_per_wg;
+  int64_t n_ublocks;
+  int64_t n_users_pad;
+  int n_chunks;
+  int64_t chunk_items;
+  int grid;
+  size_t cand_bytes;
+  size_t cnt_bytes;
+};
+
+// Launch the scan for rows of width W (bf16 units) on stream s; defined per
+// dtype in score_scan_bf16.hip / score_scan_f32.hip. Returns false for a
+// (W, cap) pair that has no instantiation.
+bool launch_scan_bf16(const Plan& p, const TopkArgs& a, int w, bool seeded, hipStream_t s);
+bool launch_scan_f32(const Plan& p, const TopkArgs& a, int w, bool seeded, hipStream_t s);
+
+// Instantiate and launch one dtype's scan over the supported widths.
+template <bool F32, int... Ws>
+bool launch_scan_widths(const Plan& p, const TopkArgs& a, int w, bool seeded, hipStream_t s) {
+  bool done = false;
+  auto one = [&](auto WC) {
+    constexpr int WW = decltype(WC)::value;
+    if (done || w != WW) return;
+    done = true;
+#define DR_SCAN(CC, SD) \
+  hipLaunchKernelGGL((score_scan_kernel<WW, CC, SD, F32>), dim3(p.grid), dim3(kThreads), 0, s, a)
+    if (p.cap == 512) {
+      if (seeded) DR_SCAN(512, true); else DR_SCAN(512, false);
+    } else if (p.cap == 1024) {
+      if (seeded) DR_SCAN(1024, true); else DR_SCAN(1024, false);
+    } else if (p.cap == 2048) {
+      if (seeded) DR_SCAN(2048, true); else DR_SCAN(2048, false);
+    } else {
+      done = false;
+    }
+#undef DR_SCAN
+  };
+  (one(IC<Ws>{}), ...);
+  return done;
+}
+
+}  // namespace dr_topk

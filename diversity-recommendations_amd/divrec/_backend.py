@@ -39,10 +39,10 @@ SIGNATURES = {
     "dr_last_error": (ctypes.c_char_p, []),
     "dr_gather_dot": (_i32, [_p, _p, _i32, _i64, _p, _p, _i64, _p, _p]),
     "dr_gather_dot_backward": (_i32, [_p, _p, _i64, _p, _p, _i64, _p, _p, _p, _p]),
-    "dr_score_topk_workspace": (_sz, [_i64, _i64, _i32, _i32]),
+    "dr_score_topk_workspace": (_sz, [_i64, _i64, _i32, _i32, _i32]),
     "dr_score_topk": (
         _i32,
-        [_p, _p, _i64, _p, _i64, _i64, _i32, _i32, _p, _p, _p, _p, _p, _sz, _p],
+        [_p, _p, _i64, _p, _i64, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _sz, _p],
     ),
     "dr_topk_merge": (_i32, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p]),
     "dr_ild_dense": (_i32, [_p, _i32, _i64, _i32, _p, _i32, _i64, _p, _p]),

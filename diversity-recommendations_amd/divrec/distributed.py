@@ -20,9 +20,14 @@ single-device dr_score_topk over the whole catalog.
 Grid layout (``grid_layout``): the G ranks form a (G / S) x S grid. The S
 ranks of a row share one user slice and row-shard the item table S ways; the
 exchange above runs inside the row (a process group of S ranks). S = G is
-pure item sharding; S = 1 is pure user sharding (no exchange). The scan's
-survivor stream costs ~users * k * ln(items / k) per rank, so at fixed U x I
-fewer item shards mean less of it.
+pure item sharding (the north-star layout, bench.py's default); S = 1 is pure
+user sharding (no exchange). The scan's survivor stream costs
+~users * k * ln(items / k) per rank, so at fixed U x I fewer item shards mean
+less of it.
+
+User-sharded metrics (config 5: MMR re-rank + ILD):
+every rank owns a user slice and the whole (replicated) item table; the only
+collective is ``global_mean``, one all_reduce of (sum, count).
 """
 from __future__ import annotations
 
@@ -105,6 +110,20 @@ def exchange_partials(scores: torch.Tensor, items: torch.Tensor, group=None) -> 
         out = out.to(scores.device)
     out = out.view(world, n_r, k, 2)
     return out[..., 0].contiguous().view(torch.float32), out[..., 1].contiguous()
+
+
+def global_mean(values: torch.Tensor, group=None) -> torch.Tensor:
+    """Mean of per-user values (e.g. ILD) held by the ranks of ``group``, each
+    for its own user slice: ONE all_reduce of the float64 (sum, count) pair.
+    Equals ScoreWithReduction's 'mean' (sum / size, base_losses.py:22-27) over
+    the concatenated values up to fp32 rounding of the final quotient."""
+    t = torch.stack([values.detach().to(torch.float64).sum(),
+                     torch.tensor(float(values.numel()), dtype=torch.float64,
+                                  device=values.device)])
+    staged = t.is_cuda and dist.get_backend(group) == "gloo"
+    src = t.cpu() if staged else t
+    dist.all_reduce(src, group=group)
+    return (src[0] / src[1]).to(torch.float32).to(values.device)
 
 
 def sharded_score_topk(

@@ -30,7 +30,9 @@ from .base_losses import DatasetAwareLoss, RecommendationsAwareLoss
 class EmbeddingDistance:
     """Lazy D from item embeddings (computed per pair inside the kernel).
 
-    The kernel reads a bf16 table; a float table is rounded to bf16 once."""
+    The kernel reads a bf16 table; a float table is rounded to bf16 once, and
+    a width without a kernel instance (e.g. the reference experiments' 100) is
+    zero-padded once."""
 
     KINDS = ("cosine", "dot", "euclidean")
 
@@ -45,6 +47,8 @@ class EmbeddingDistance:
         t = self._dev_table
         if t is None or t.device != device:
             t = self.item_table.detach().to(device=device, dtype=torch.bfloat16).contiguous()
+            # widths without a kernel instance: zero columns change no distance
+            t = ops.pad_columns(t, ops._width_of(ops.ILD_WIDTHS, t.size(1), "embedding ILD"))
             self._dev_table = t
         return t
 

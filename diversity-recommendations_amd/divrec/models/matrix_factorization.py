@@ -7,8 +7,17 @@ gather + row dot of libdivrec_hip (dr_gather_dot) with its backward
 (dr_gather_dot_backward) into dense fp32 gradients; parameters must live on a
 ROCm device (``model.to("cuda")``) — there is no CPU path.
 
-New, non-breaking: ``score_topk`` — full-catalog bf16 MFMA scoring with a
-fused top-k (dr_score_topk), the hot path of get_model_recommendations.
+New, non-breaking: ``score_topk`` — full-catalog MFMA scoring with a fused
+top-k (dr_score_topk), the hot path of get_model_recommendations. Two
+precisions:
+  * ``"fp32"`` (default): the fp32 parameters themselves, scored on
+    v_mfma_f32_32x32x2_f32 — each score an exact fp32 fmaf chain, i.e. the
+    reference's fp32 arithmetic (matrix_factorization.py:26-28) up to the
+    summation order;
+  * ``"bf16"``: bf16 copies of the tables on the bf16 MFMA (16x the rate),
+    ranking the tables' bf16 rounding — the explicit fast mode.
+Any ``embedding_dim`` works: widths without a scan instance (e.g. the
+reference experiments' 100) are zero-padded once per parameter version.
 """
 from __future__ import annotations
 
@@ -19,6 +28,8 @@ import torch
 from divrec import ops
 
 from .base_models import RankingModel
+
+PRECISIONS = {"fp32": torch.float32, "bf16": torch.bfloat16}
 
 
 class _GatherDot(torch.autograd.Function):
@@ -51,7 +62,7 @@ class MatrixFactorization(RankingModel):
         self.embedding_dim = embedding_dim
         self.user_embeddings = torch.nn.Embedding(no_users, embedding_dim)
         self.item_embeddings = torch.nn.Embedding(no_items, embedding_dim)
-        self._bf16 = None  # (key, user_bf16, item_bf16) cache for score_topk
+        self._tables = {}  # precision -> (key, user table, item table) for score_topk
 
     def _device(self) -> torch.device:
         dev = self.user_embeddings.weight.device
@@ -74,16 +85,32 @@ class MatrixFactorization(RankingModel):
         iid = _on_device(dev, item_id)
         return _GatherDot.apply(self.user_embeddings.weight, self.item_embeddings.weight, uid, iid)
 
-    def bf16_tables(self) -> Tuple[torch.Tensor, torch.Tensor]:
-        """bf16 copies of both tables (re-made only when a parameter changed)."""
+    def scoring_tables(self, precision: str = "fp32") -> Tuple[torch.Tensor, torch.Tensor]:
+        """The (user, item) tables score_topk scans at ``precision``: the
+        parameters themselves when their dtype and width already have a scan
+        instance, else a converted / zero-padded copy, re-made only when a
+        parameter changed (keyed on storage and autograd version; the fused
+        optimizer steps bump the version, train/utils.py)."""
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
         self._device()
         U, I = self.user_embeddings.weight, self.item_embeddings.weight
-        key = (U.data_ptr(), U._version, I.data_ptr(), I._version)
-        if self._bf16 is None or self._bf16[0] != key:
+        dt = PRECISIONS[precision]
+        w = ops.score_width(dt, U.size(1))
+        if dt == U.dtype and w == U.size(1) and U.is_contiguous() and I.is_contiguous():
+            return U.detach(), I.detach()
+        key = (U.data_ptr(), U._version, I.data_ptr(), I._version, U.dtype)
+        hit = self._tables.get(precision)
+        if hit is None or hit[0] != key:
             with torch.no_grad():
-                self._bf16 = (key, U.detach().to(torch.bfloat16).contiguous(),
-                              I.detach().to(torch.bfloat16).contiguous())
-        return self._bf16[1], self._bf16[2]
+                hit = (key, ops.pad_columns(U.detach().to(dt).contiguous(), w),
+                       ops.pad_columns(I.detach().to(dt).contiguous(), w))
+            self._tables[precision] = hit
+        return hit[1], hit[2]
+
+    def bf16_tables(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """bf16 copies of both tables (the fast scoring mode's operands)."""
+        return self.scoring_tables("bf16")
 
     @torch.no_grad()
     def score_topk(
@@ -91,13 +118,19 @@ class MatrixFactorization(RankingModel):
         k: int,
         user_ids: Optional[torch.Tensor] = None,
         exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+        precision: str = "fp32",
+        n_items: Optional[int] = None,
     ) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Top-k items of each user (all users, or ``user_ids``) over the whole
-        catalog: (items int64 [n, k], scores fp32 [n, k]) on the model's
-        device, ordered by score desc then item id asc. ``exclude`` =
-        (rowptr int64 [n+1], items int32) CSR of items never to return."""
+        """Top-k items of each user (all users, or ``user_ids``) over the
+        catalog (the first ``n_items`` item rows; default all): (items int64
+        [n, k], scores fp32 [n, k]) on the model's device, ordered by score
+        desc then item id asc. ``exclude`` = (rowptr int64 [n+1], items int32)
+        CSR of items never to return. ``precision`` "fp32" (default, the
+        reference's arithmetic) or "bf16" (fast mode)."""
         dev = self._device()
-        U, I = self.bf16_tables()
+        U, I = self.scoring_tables(precision)
+        if n_items is not None:
+            I = I[: int(n_items)]
         uids = None if user_ids is None else _on_device(dev, user_ids)
         ex = None
         if exclude is not None:

@@ -81,6 +81,33 @@ def gather_dot_backward(
 
 
 # --------------------------------------------------------------------------- top-K
+# Widths with a scan instantiation per table dtype (include/divrec_hip.h); any
+# other width is served by zero-padding both tables (zero columns add exact
+# zeros to every dot product).
+SCORE_WIDTHS = {torch.bfloat16: (32, 64, 128, 256, 512), torch.float32: (32, 64, 128, 256)}
+
+
+def score_width(dtype: torch.dtype, d: int) -> int:
+    """The scan width an embedding of width ``d`` runs at (d itself or the
+    next supported width, reached by zero-padding)."""
+    _need(dtype in SCORE_WIDTHS, "score_topk tables must be bf16 or fp32")
+    for w in SCORE_WIDTHS[dtype]:
+        if d <= w:
+            return w
+    raise ValueError(f"embedding_dim {d} is wider than the widest {dtype} scan "
+                     f"({SCORE_WIDTHS[dtype][-1]})")
+
+
+def pad_columns(table: torch.Tensor, width: int) -> torch.Tensor:
+    """``table`` [rows, d] widened to ``width`` columns with zeros (a copy);
+    the table itself when it already has that width."""
+    if table.size(1) == width:
+        return table
+    out = torch.zeros((table.size(0), width), dtype=table.dtype, device=table.device)
+    out[:, :table.size(1)] = table
+    return out
+
+
 def score_topk(
     user_table: torch.Tensor,
     item_table: torch.Tensor,
@@ -91,7 +118,13 @@ def score_topk(
     exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Top-k items per user over the catalog slice ``item_table`` (global ids
-    ``item_base + row``) by bf16 MFMA scores; order = score desc, item id asc.
+    ``item_base + row``); order = score desc, item id asc.
+
+    The tables' dtype picks the arithmetic: bf16 tables run the bf16 MFMA scan
+    (exact products, fp32 sums: the fast mode), fp32 tables the fp32 MFMA scan
+    (an exact fp32 fmaf chain per score: the reference's arithmetic up to the
+    summation order). Widths without a scan instance are zero-padded here (a
+    copy per call; MatrixFactorization caches its padded tables).
 
     ``user_ids`` (int64) selects user rows; if None the first ``n_users`` rows
     (default: all) are scored. ``exclude = (rowptr int64 [n+1], items int32)``
@@ -99,13 +132,14 @@ def score_topk(
     Returns (scores fp32 [n, k], items int32 [n, k]).
     """
     dev = B.require_device(user_table, item_table, user_ids)
-    _need(user_table.dtype == torch.bfloat16 and item_table.dtype == torch.bfloat16,
-          "score_topk runs on bf16 tables (convert with .to(torch.bfloat16))")
+    _need(user_table.dtype == item_table.dtype and user_table.dtype in SCORE_WIDTHS,
+          "score_topk tables must both be bf16 or both fp32")
     _need(user_table.dim() == 2 and item_table.dim() == 2, "tables must be 2-D")
     d = user_table.size(1)
     _need(item_table.size(1) == d, "tables must share embedding_dim")
-    _need(d in (32, 64, 128, 256), "embedding_dim must be one of 32, 64, 128, 256")
     _contig(user_table, "user_table"), _contig(item_table, "item_table")
+    w = score_width(user_table.dtype, d)
+    user_table, item_table = pad_columns(user_table, w), pad_columns(item_table, w)
     _need(1 <= k <= 1024, "k must be in [1, 1024]")
     if user_ids is not None:
         _need(user_ids.dtype == torch.int64 and user_ids.dim() == 1, "user_ids must be 1-D int64")
@@ -133,11 +167,12 @@ def score_topk(
     if n == 0:
         return scores, items
     L = B.lib()
-    ws_bytes = L.dr_score_topk_workspace(n, n_items, d, k)
+    dt = B.dtype_code(user_table.dtype)
+    ws_bytes = L.dr_score_topk_workspace(n, n_items, dt, w, k)
     ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=dev)
     rc = L.dr_score_topk(
         user_table.data_ptr(), B.ptr(user_ids), n, item_table.data_ptr(), n_items, int(item_base),
-        d, int(k), B.ptr(rowptr), B.ptr(cols), scores.data_ptr(), items.data_ptr(),
+        dt, w, int(k), B.ptr(rowptr), B.ptr(cols), scores.data_ptr(), items.data_ptr(),
         ws.data_ptr(), ws.numel(), B.stream(dev),
     )
     B.check(rc, "dr_score_topk")
@@ -153,7 +188,8 @@ def topk_merge(
     _need(scores.dtype == torch.float32 and items.dtype == torch.int32, "fp32 scores, int32 items")
     parts, n, k_in = scores.shape
     k_out = k_in if k_out is None else int(k_out)
-    _need(1 <= k_out <= parts * k_in and parts * k_in <= 2048, "k_out / parts*k_in out of range")
+    _need(1 <= k_out <= parts * k_in, "k_out must be in [1, parts * k_in]")
+    _need(parts * k_in <= 2048 or k_out <= 1024, "k_out must be <= 1024 when parts * k_in > 2048")
     out_s = torch.empty((n, k_out), dtype=torch.float32, device=dev)
     out_i = torch.empty((n, k_out), dtype=torch.int32, device=dev)
     if n == 0:
@@ -212,6 +248,15 @@ def ild_labels(recs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
 
 
 _KINDS = {"cosine": B.DR_ILD_COSINE, "dot": B.DR_ILD_DOT, "euclidean": B.DR_ILD_EUCLIDEAN}
+ILD_WIDTHS = (32, 64, 128, 256)  # dr_ild_embedding instances; others are zero-padded
+MMR_WIDTHS = (64, 128)           # dr_mmr_rerank instances; others are zero-padded
+
+
+def _width_of(widths, d: int, what: str) -> int:
+    for w in widths:
+        if d <= w:
+            return w
+    raise ValueError(f"{what} supports embedding_dim <= {widths[-1]}, got {d}")
 
 
 def ild_embedding(recs: torch.Tensor, item_table: torch.Tensor, kind: str = "cosine") -> torch.Tensor:
@@ -221,6 +266,7 @@ def ild_embedding(recs: torch.Tensor, item_table: torch.Tensor, kind: str = "cos
     _need(item_table.dtype == torch.bfloat16 and item_table.dim() == 2, "item_table must be bf16 2-D")
     _contig(item_table, "item_table")
     _need(kind in _KINDS, f"kind must be one of {sorted(_KINDS)}")
+    item_table = pad_columns(item_table, _width_of(ILD_WIDTHS, item_table.size(1), "embedding ILD"))
     n, k = recs.shape
     _need(k <= 128, "embedding ILD supports k <= 128")
     out = torch.empty(n, dtype=torch.float32, device=dev)
@@ -367,8 +413,9 @@ def mmr_rerank(
     _need(cand_items.dtype == torch.int32 and cand_scores.dtype == torch.float32,
           "int32 candidate ids, fp32 scores")
     _need(cand_items.dim() == 2 and cand_items.shape == cand_scores.shape, "[n, C] inputs")
-    _need(item_table.dtype == torch.bfloat16 and item_table.size(1) in (64, 128),
-          "item_table must be bf16 with d in {64, 128}")
+    _need(item_table.dtype == torch.bfloat16 and item_table.dim() == 2, "item_table must be bf16 2-D")
+    item_table = pad_columns(item_table.contiguous(),
+                             _width_of(MMR_WIDTHS, item_table.size(1), "mmr_rerank"))
     n, C = cand_items.shape
     out = torch.empty((n, int(k_out)), dtype=torch.int32, device=dev)
     if n == 0:

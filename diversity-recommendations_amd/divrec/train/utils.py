@@ -3,10 +3,11 @@
 Same functions, arguments and return values as the reference. On the hot path:
 
 * ``get_model_recommendations`` with a MatrixFactorization model runs ONE
-  dr_score_topk over all users (bf16 MFMA scores, fused top-k, frozen items
-  excluded through a CSR) instead of the reference's per-user loop of set
-  differences, full-catalog forward and full argsort (:58-77). Ties are broken
-  by item id ascending (the reference's argsort is unstable there, :73).
+  dr_score_topk over all users (fp32 MFMA scores by default, fused top-k,
+  frozen items excluded through a CSR) instead of the reference's per-user
+  loop of set differences, full-catalog forward and full argsort (:58-77).
+  Ties are broken by item id ascending (the reference's argsort is unstable
+  there, :73).
 * ``pair_wise_train_loop`` with MatrixFactorization + LogSigmoidDifferenceLoss
   runs each batch as ONE dr_bpr_fwd_bwd (gather, loss, AUC flags and dense
   embedding gradients fused) followed by dr_adam_dense when the optimizer is a
@@ -19,6 +20,8 @@ from __future__ import annotations
 from typing import List, Optional, Tuple
 
 import torch
+
+from torch.autograd.graph import increment_version
 
 from divrec import ops
 from divrec.datasets import PairWiseDataset, PointWiseDataset, RankingDataset
@@ -71,16 +74,50 @@ def pair_wise_score_loop(dataset: PairWiseDataset, model: RankingModel,
             for loss in losses]
 
 
+def _mf_scoring(model: RankingModel) -> bool:
+    """The MF fast path applies only to MatrixFactorization's own forward: a
+    subclass that overrides forward is scored through its forward."""
+    return (isinstance(model, MatrixFactorization)
+            and type(model).forward is MatrixFactorization.forward)
+
+
+def _list_length(dataset: RankingDataset, excl, n_users: int, n_items: int, k: int) -> int:
+    """Length of the reference's recommendation lists: min(k, candidates),
+    where the candidates of a user are the catalog minus its frozen items.
+    Lists of different lengths make the reference's torch.LongTensor(...)
+    raise (utils.py:77); so does this."""
+    if excl is None:
+        return min(k, n_items)
+    rowptr, cols = excl
+    inside = (cols.to(torch.int64) < n_items).to(torch.int64)
+    csum = torch.zeros(cols.numel() + 1, dtype=torch.int64)
+    csum[1:] = torch.cumsum(inside, 0)
+    n_cands = n_items - (csum[rowptr[1:]] - csum[rowptr[:-1]])
+    lengths = torch.clamp(n_cands, max=k)
+    lo, hi = int(lengths.min()), int(lengths.max())
+    if lo != hi:
+        raise ValueError(f"expected sequence of length {hi} at dim 1 (got {lo}): a user has "
+                         f"fewer than {k} candidates, so the recommendation lists are ragged")
+    return lo
+
+
 def get_model_recommendations(dataset: RankingDataset, model: RankingModel,
                               number_of_recommendations: int) -> torch.LongTensor:
     """Top-``number_of_recommendations`` candidates of every user of
-    ``dataset`` (LongTensor [U, k] on the CPU, like the reference)."""
+    ``dataset`` (LongTensor [U, k] on the CPU, like the reference), scored in
+    fp32 (MatrixFactorization.score_topk's faithful mode)."""
     k = int(number_of_recommendations)
     n_users = int(dataset.data.number_of_users)
-    if isinstance(model, MatrixFactorization):
-        user_ids = None if n_users == model.no_users else torch.arange(n_users)
+    n_items = int(dataset.data.number_of_items)
+    if _mf_scoring(model) and n_users <= model.no_users and n_items <= model.no_items:
+        if n_users == 0:
+            return torch.LongTensor([])
         excl = dataset.exclusion_csr()
-        items, _ = model.score_topk(k, user_ids=user_ids, exclude=excl)
+        k_len = _list_length(dataset, excl, n_users, n_items, k)
+        if k_len == 0:
+            return torch.zeros((n_users, 0), dtype=torch.int64)
+        user_ids = None if n_users == model.no_users else torch.arange(n_users)
+        items, _ = model.score_topk(k_len, user_ids=user_ids, exclude=excl, n_items=n_items)
         return items.cpu()
     # Generic RankingModel: the reference loop (model scores per user), with
     # the deterministic tie-break. Outside the MF hot path.
@@ -154,6 +191,10 @@ def fused_adam_step(optimizer: torch.optim.Adam) -> None:
             st["step"] += 1
             ops.adam_dense(p.data, p.grad, st["exp_avg"], st["exp_avg_sq"], group["lr"], beta1,
                            beta2, group["eps"], group["weight_decay"], int(st["step"].item()))
+            # the kernel wrote p through a raw pointer: bump its autograd
+            # version so caches keyed on it (MatrixFactorization's scoring
+            # tables) see the change, as after a torch in-place update
+            increment_version(p)
 
 
 def _plain_sparse_adam(optimizer: torch.optim.Optimizer) -> bool:
@@ -183,6 +224,7 @@ def lazy_adam_step(optimizer: torch.optim.SparseAdam, rows: dict) -> None:
             st["step"] += 1
             ops.adam_rows(p.data, p.grad, st["exp_avg"], st["exp_avg_sq"], rows[p],
                           group["lr"], beta1, beta2, group["eps"], st["step"])
+            increment_version(p)  # raw-pointer update, as in fused_adam_step
 
 
 def _bpr_fast_path(model, loss, scores) -> bool:
@@ -224,9 +266,9 @@ def pair_wise_train_loop(dataset: PairWiseDataset, model: RankingModel, loss: Pa
                 optimizer.step()
                 optimizer.zero_grad()
             batch_losses.append(loss_value.detach())
-            if n_scores:
-                auc = torch.sum(hits.float(), dim=0) / B
-                batch_scores.append(torch.stack([auc] * n_scores))
+            if n_scores:  # AUCScore.pair_wise = the hit flags, reduced as each score says
+                batch_scores.append(torch.stack(
+                    [s.reduce_loss_values(hits).double() for s in scores]))
         else:
             positives = model(user_id, pos, uf, pf)
             negatives = model(user_id, neg, uf, nf)
@@ -237,7 +279,7 @@ def pair_wise_train_loop(dataset: PairWiseDataset, model: RankingModel, loss: Pa
             batch_losses.append(loss_value.detach())
             if n_scores:
                 batch_scores.append(torch.stack(
-                    [s(positives.detach(), negatives.detach()).float() for s in scores]))
+                    [s(positives.detach(), negatives.detach()).double() for s in scores]))
     count = len(batch_losses)
     # per-batch values summed as Python floats in batch order, like the reference
     mean_loss = sum(float(v) for v in torch.stack(batch_losses).double().cpu().tolist()) / count

@@ -72,16 +72,23 @@ int dr_gather_dot_backward(const float* user_table, const float* item_table, int
 /* ---------------------------------------------------------------------------
  * Full-catalog scoring + top-K: for each of the n_users user rows, the k best
  * items of the catalog slice [item_base, item_base + n_items) by
- * score = <U[user], I[item]> computed as a bf16 MFMA GEMM with fp32
- * accumulation. Replaces get_model_recommendations (divrec/train/utils.py:53-77)
- * over RankingDataset candidates (divrec/datasets/base_datasets.py:136-171).
+ * score = <U[user], I[item]>. Replaces get_model_recommendations
+ * (divrec/train/utils.py:53-77) over RankingDataset candidates
+ * (divrec/datasets/base_datasets.py:136-171), which scores each candidate with
+ * MatrixFactorization.forward (divrec/models/matrix_factorization.py:26-28).
  *
  * Ranking order is score descending, item id ascending (the deterministic
  * tie-break the reference's unstable argsort leaves undefined, utils.py:73).
  *
- *   user_table  bf16 [*, d]; user_ids int64 [n_users] or NULL (rows 0..n_users-1)
- *   item_table  bf16 [n_items, d] (the rows of THIS slice; global id = item_base + row)
- *   d in {32, 64, 128, 256}; 1 <= k <= 1024
+ *   dtype       DR_BF16: bf16 tables, bf16 MFMA (exact products, fp32 sums) —
+ *               the fast mode; d in {32, 64, 128, 256, 512}.
+ *               DR_F32: fp32 tables, fp32 MFMA (an exact fp32 fmaf chain per
+ *               score, the reference's own arithmetic up to summation order) —
+ *               the faithful mode; d in {32, 64, 128, 256}.
+ *               Other widths: pad both tables with zero columns (exact).
+ *   user_table  [*, d]; user_ids int64 [n_users] or NULL (rows 0..n_users-1)
+ *   item_table  [n_items, d] (the rows of THIS slice; global id = item_base + row)
+ *   1 <= k <= 1024
  *   excl_rowptr int64 [n_users + 1], excl_items int32 (GLOBAL item ids, sorted
  *     ascending per row): items excluded per user (RankingDataset `frozen`,
  *     base_datasets.py:143-149). Both NULL = no exclusion.
@@ -89,17 +96,18 @@ int dr_gather_dot_backward(const float* user_table, const float* item_table, int
  *     slots with no candidate hold item -1 and score -inf.
  *   workspace of dr_score_topk_workspace(...) bytes (query with identical args).
  */
-size_t dr_score_topk_workspace(int64_t n_users, int64_t n_items, int d, int k);
+size_t dr_score_topk_workspace(int64_t n_users, int64_t n_items, int dtype, int d, int k);
 int dr_score_topk(const void* user_table, const int64_t* user_ids, int64_t n_users,
-                  const void* item_table, int64_t n_items, int64_t item_base, int d, int k,
-                  const int64_t* excl_rowptr, const int32_t* excl_items, float* out_scores,
-                  int32_t* out_items, void* workspace, size_t workspace_bytes,
-                  dr_stream_t stream);
+                  const void* item_table, int64_t n_items, int64_t item_base, int dtype, int d,
+                  int k, const int64_t* excl_rowptr, const int32_t* excl_items,
+                  float* out_scores, int32_t* out_items, void* workspace,
+                  size_t workspace_bytes, dr_stream_t stream);
 
 /* Merge `parts` per-user top-k lists (each sorted by the order above) into one:
- *   in_scores/in_items [parts, n_users, k_in] -> out [n_users, k_out], k_out <= parts*k_in.
+ *   in_scores/in_items [parts, n_users, k_in] -> out [n_users, k_out], k_out <= parts*k_in
+ *   (k_out <= 1024 when parts*k_in > 2048; entries with item -1 are empty).
  * This is the exchange step of the item-row-sharded top-K:
- * shard partials are all-gathered over RCCL and merged here; the result is
+ * shard partials are exchanged over RCCL and merged here; the result is
  * bit-identical to the single-device dr_score_topk over the whole catalog. */
 int dr_topk_merge(const float* in_scores, const int32_t* in_items, int parts, int64_t n_users,
                   int k_in, int k_out, float* out_scores, int32_t* out_items,

@@ -19,6 +19,10 @@ Fixtures (one .npz each):
                   (train/utils.py:130-164, losses/log_sigmoid_difference_loss.py:11-14)
   bpr_loop        pair_wise_train_loop over a seeded PairWiseDataset (random.choices)
   ml100k_cfg1     config 1: ML-100K-shaped synthetic MF d=32 top-10 + ILD
+  recs_fp32_d100_* get_model_recommendations with raw N(0,1) fp32 weights (the
+                  nn.Embedding init, no bf16 rounding) at the reference
+                  experiments' embedding_dim 100, k = 10 / 100 / 1000
+  ml100k_d100     config 1 at d=100 with raw fp32 weights: top-10 + ILD + metrics
 """
 from __future__ import annotations
 
@@ -240,6 +244,48 @@ def main():
         pri = metrics.PRI(dataset=full_ds)(test_inter, recs)
         mapk = metrics.MeanAveragePrecisionAtKScore()(test_inter, recs)
     save("ml100k_cfg1", U=U, I=I, train=tr, test=te, recs=recs, ild=res[0], precision=prec,
+         recall=rec, ap=ap, ndcg=ndcg, entropy=ent, pri=pri, map=mapk)
+
+    # ---------------------------------------------------------------- raw fp32 weights, d=100
+    # The reference experiments train MatrixFactorization at embedding_dim 100
+    # (experiments/experiments/movie_lens_100k_mf_bpr/config.yaml:7) from
+    # nn.Embedding's N(0,1) init: fp32 values that bf16 does not represent.
+    g = torch.Generator().manual_seed(4321)
+    U = torch.randn(64, 100, generator=g)
+    I = torch.randn(2000, 100, generator=g)
+    for k in (10, 100, 1000):
+        run_recs(f"recs_fp32_d100_k{k}", U, I, k, stable_ties=False)
+
+    g = torch.Generator().manual_seed(943)
+    nu, ni, d = 943, 1682, 100
+    U = torch.randn(nu, d, generator=g)
+    I = torch.randn(ni, d, generator=g)
+    rng = np.random.default_rng(943)
+    tr, te = synthetic_split(rng, nu, ni, 96, 10)
+    train_ds = datasets.UserItemInteractionsDataset(tr, number_of_users=nu, number_of_items=ni)
+    test_ds = datasets.UserItemInteractionsDataset(te, number_of_users=nu, number_of_items=ni)
+    mf = models.MatrixFactorization(nu, ni, d)
+    with torch.no_grad():
+        mf.user_embeddings.weight.copy_(U)
+        mf.item_embeddings.weight.copy_(I)
+    rds = datasets.RankingDataset(test_ds, frozen=train_ds)
+    En = I / I.norm(dim=1, keepdim=True)
+    Dc = 1.0 - En @ En.T
+    ild = losses.IntraListDiversityScore(distance_matrix=Dc, reduction="none")
+    with torch.no_grad():
+        res = train.recommendations_score_loop(rds, mf, [ild], 10)
+        recs = train.get_model_recommendations(rds, mf, 10)
+    full_ds = datasets.UserItemInteractionsDataset(torch.cat([tr, te]), number_of_users=nu,
+                                                   number_of_items=ni)
+    with torch.no_grad():
+        prec = metrics.precision_at_k(te, recs)
+        rec = metrics.recall_at_k(te, recs)
+        ap = metrics.average_precision_at_k(te, recs)
+        ndcg = metrics.normalized_discounted_cumulative_gain(te, recs)
+        ent = metrics.EntropyDiversityScore(dataset=full_ds)(te, recs)
+        pri = metrics.PRI(dataset=full_ds)(te, recs)
+        mapk = metrics.MeanAveragePrecisionAtKScore()(te, recs)
+    save("ml100k_d100", U=U, I=I, train=tr, test=te, recs=recs, ild=res[0], precision=prec,
          recall=rec, ap=ap, ndcg=ndcg, entropy=ent, pri=pri, map=mapk)
 
 

@@ -18,6 +18,7 @@ import torch
 
 import oracle
 from divrec import datasets, losses, metrics, models, ops, train
+from topk_checks import fp32_row_tol, gap_check
 from divrec.losses import EmbeddingDistance, LabelEquality
 
 pytestmark = pytest.mark.gpu
@@ -110,6 +111,112 @@ def test_recommendations_float_gap_exact(name):
     tol = 1e-5 * max(1.0, float(np.abs(U).max() * np.abs(I).max() * U.shape[1] / 8))
     bad = assert_topk_gap_exact(recs, g["recs"], U, I, (rowptr.numpy(), cols.numpy()), tol)
     assert bad <= U.shape[0] // 16
+
+
+@pytest.mark.parametrize("name", ["recs_fp32_d100_k10", "recs_fp32_d100_k100",
+                                  "recs_fp32_d100_k1000"])
+def test_recommendations_raw_fp32_d100(name):
+    """The reference's own model configuration: embedding_dim 100 (the
+    experiments' config.yaml:7) and raw N(0,1) fp32 weights. The default
+    (fp32-faithful) scoring equals the reference's lists except at near-ties
+    of the exact scores (fp32 tolerance, tests/topk_checks.py)."""
+    g = load(name)
+    U, I, k = g["U"], g["I"], int(g["k"])
+    rds = ranking_dataset(g, U.shape[0], I.shape[0])
+    recs = train.get_model_recommendations(rds, mf_from(U, I), k)
+    assert recs.dtype == torch.int64 and recs.shape == (U.shape[0], k)
+    rowptr, cols = rds.exclusion_csr()
+    bad = gap_check(recs.numpy(), g["recs"], U, I, (rowptr.numpy(), cols.numpy()),
+                    fp32_row_tol(U, I))
+    assert bad <= max(1, U.shape[0] // 32)
+
+
+def test_recommendations_bf16_mode_is_explicit():
+    """precision='bf16' ranks the tables' bf16 rounding (the fast mode): on
+    raw fp32 weights it is NOT the reference's ranking, which is why fp32 is
+    the default. Its lists equal the fp32 scan of the bf16-rounded tables."""
+    g = load("recs_fp32_d100_k100")
+    U, I = g["U"], g["I"]
+    mf = mf_from(U, I)
+    rds = ranking_dataset(g, U.shape[0], I.shape[0])
+    excl = rds.exclusion_csr()
+    items16, _ = mf.score_topk(100, exclude=excl, precision="bf16")
+    rounded = mf_from(oracle.as_bf16_f32(U), oracle.as_bf16_f32(I))
+    items32, _ = rounded.score_topk(100, exclude=excl, precision="fp32")
+    assert torch.equal(items16, items32)
+    assert (items16.cpu().numpy() != g["recs"]).any(axis=1).sum() > 0
+
+
+def test_ml100k_d100_end_to_end():
+    """configs[0] at the reference experiments' width: d=100, raw fp32 weights,
+    top-10 + dense cosine ILD + accuracy / diversity metrics through
+    recommendations_score_loop."""
+    g = load("ml100k_d100")
+    U, I = g["U"], g["I"]
+    nu, ni = U.shape[0], I.shape[0]
+    rds = ranking_dataset(g, nu, ni)
+    mf = mf_from(U, I)
+    It = torch.from_numpy(I)
+    En = It / It.norm(dim=1, keepdim=True)
+    ild = losses.IntraListDiversityScore(distance_matrix=1.0 - En @ En.T, reduction="none")
+    te = torch.from_numpy(g["test"])
+    res = train.recommendations_score_loop(rds, mf, [ild], 10)
+    recs = train.get_model_recommendations(rds, mf, 10).numpy()
+    rowptr, cols = rds.exclusion_csr()
+    bad = gap_check(recs, g["recs"], U, I, (rowptr.numpy(), cols.numpy()), fp32_row_tol(U, I))
+    assert bad <= nu // 100
+    same = (recs == g["recs"]).all(axis=1)
+    assert np.array_equal(res[0].cpu().numpy()[same], g["ild"][same])
+    lazy = losses.IntraListDiversityScore(distance_matrix=EmbeddingDistance(It, "cosine"),
+                                          reduction="none")  # d=100 zero-padded, bf16 Gram
+    ref_recs = torch.from_numpy(g["recs"])
+    assert np.allclose(lazy(None, ref_recs).cpu().numpy(), g["ild"], rtol=2e-3, atol=2e-3)
+    for fn, key in ((metrics.precision_at_k, "precision"), (metrics.recall_at_k, "recall"),
+                    (metrics.average_precision_at_k, "ap"),
+                    (metrics.normalized_discounted_cumulative_gain, "ndcg")):
+        assert np.allclose(fn(te, ref_recs).cpu().numpy(), g[key], rtol=1e-6, atol=1e-7), key
+
+
+def test_scoring_tables_follow_fused_training():
+    """train -> recommend -> train -> recommend: the fused Adam steps write the
+    parameters through raw pointers; the scoring tables (cached padded fp32 at
+    d=100, cached bf16) must follow them (the version bump in fused_adam_step)."""
+    rng = np.random.default_rng(61)
+    nu, ni, d = 30, 200, 100
+    inter = np.stack([rng.integers(0, nu, 600), rng.integers(0, ni, 600)], axis=1)
+    data = datasets.UserItemInteractionsDataset(
+        torch.from_numpy(inter).long(), number_of_users=nu, number_of_items=ni,
+        user_features=datasets.Features(torch.zeros(nu, 1), ["x"]),
+        item_features=datasets.Features(torch.zeros(ni, 1), ["x"]))
+    rds = datasets.RankingDataset(data, frozen=data)
+    torch.manual_seed(2)
+    mf = models.MatrixFactorization(nu, ni, d).to(DEV)
+    opt = torch.optim.Adam(mf.parameters(), lr=5e-2)
+    for precision in ("fp32", "bf16", "fp32"):
+        random.seed(3)
+        train.pair_wise_train_loop(datasets.PairWiseDataset(data, max_sampled=4), mf,
+                                   losses.LogSigmoidDifferenceLoss(), opt, batch_size=64)
+        got, _ = mf.score_topk(10, exclude=rds.exclusion_csr(), precision=precision)
+        fresh = mf_from(mf.user_embeddings.weight.detach().cpu().numpy(),
+                        mf.item_embeddings.weight.detach().cpu().numpy())
+        want, _ = fresh.score_topk(10, exclude=rds.exclusion_csr(), precision=precision)
+        assert torch.equal(got, want), precision
+
+
+def test_recommendations_ragged_lists_raise_like_reference():
+    """A user with fewer candidates than k: the reference's
+    torch.LongTensor(recommendations) raises on ragged lists (utils.py:77);
+    equal short lists come back short."""
+    train_ds = datasets.UserItemInteractionsDataset(torch.LongTensor([[0, 1], [0, 2], [1, 3]]),
+                                                    number_of_users=2, number_of_items=5)
+    test_ds = datasets.UserItemInteractionsDataset(torch.LongTensor([[0, 0], [1, 0]]),
+                                                   number_of_users=2, number_of_items=5)
+    mf = models.MatrixFactorization(2, 5, 32).to(DEV)
+    with pytest.raises(ValueError):
+        train.get_model_recommendations(datasets.RankingDataset(test_ds, frozen=train_ds), mf, 4)
+    recs = train.get_model_recommendations(datasets.RankingDataset(test_ds, frozen=train_ds), mf, 3)
+    assert recs.shape == (2, 3)
+    assert not set(recs[0].tolist()) & {1, 2} and 3 not in recs[1].tolist()
 
 
 def test_ml100k_config1_end_to_end():

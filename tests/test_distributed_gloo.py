@@ -12,7 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle
-from divrec.distributed import exchange_partials, shard_range, sharded_score_topk
+from divrec.distributed import exchange_partials, global_mean, shard_range, sharded_score_topk
 
 
 def _free_port():
@@ -150,3 +150,79 @@ def test_grid_layout_equals_single_device(world, S):
         assert np.array_equal(s, ref_s[a:b].astype(np.float32))
         owned[a:b] += 1
     assert (owned == 1).all()
+
+
+def _k1000_worker(rank, world, port, U, I, k, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from divrec.distributed import grid_layout
+        lay = grid_layout(world)  # pure item sharding: S = world, the bench default
+        lo, hi = lay.item_range(I.shape[0])
+        (s, i), (ulo, uhi) = sharded_score_topk(torch.from_numpy(U), torch.from_numpy(I[lo:hi]), lo,
+                                                k, group=lay.group, local_topk=_local_topk,
+                                                merge=_merge)
+        q.put((rank, ulo, uhi, s.numpy(), i.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_item_sharded_8_ranks_k1000():
+    """World size 8, pure 8-way item sharding (the north-star layout) at
+    k = 1000 (config 5's candidate lists): the production exchange moves
+    8 x 1000 partial entries per user; every user's merged list equals the
+    single-device top-1000."""
+    world, k = 8, 1000
+    rng = np.random.default_rng(81000)
+    U = rng.integers(-3, 4, size=(19, 8)).astype(np.float32)
+    I = rng.integers(-3, 4, size=(8 * 1100 + 5, 8)).astype(np.float32)
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, return_scores=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_k1000_worker, args=(r, world, port, U, I, k, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    owned = np.zeros(U.shape[0], dtype=int)
+    for rank, ulo, uhi, s, i in got:
+        assert (ulo, uhi) == shard_range(U.shape[0], world, rank)
+        assert np.array_equal(i, ref_i[ulo:uhi])
+        assert np.array_equal(s, ref_s[ulo:uhi].astype(np.float32))
+        owned[ulo:uhi] += 1
+    assert (owned == 1).all()
+
+
+def _mean_worker(rank, world, port, vals, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard_range(vals.size, world, rank)
+        q.put((rank, float(global_mean(torch.from_numpy(vals[lo:hi])))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_user_sharded_ild_mean():
+    """Config 5's users sharded over ranks: the mean ILD from one all_reduce of
+    (sum, count) equals the reference's 'mean' reduction (sum / size) over all
+    users, uneven slices included."""
+    world = 3
+    vals = np.random.default_rng(5).random(1001).astype(np.float32)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mean_worker, args=(r, world, port, vals, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = float(oracle.reduce_values(vals, "mean"))
+    for _, m in got:
+        assert m == pytest.approx(want, rel=1e-6)

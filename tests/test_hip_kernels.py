@@ -11,6 +11,7 @@ import torch
 
 import oracle
 from divrec import ops
+from topk_checks import fp32_row_tol, gap_check
 
 pytestmark = pytest.mark.gpu
 
@@ -245,6 +246,144 @@ def test_score_topk_float_tolerance():
     for u in range(S.shape[0]):
         must = np.nonzero(S[u] > kth[u] + 2 * tol)[0]
         assert np.isin(must, it[u]).all()
+
+
+# --------------------------------------------------------------------------- fp32-faithful scan
+def _f32(x):
+    return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(DEV)
+
+
+@pytest.mark.parametrize("d", [32, 64, 100, 128, 256])
+@pytest.mark.parametrize("k", [1, 10, 100])
+def test_score_topk_fp32_integer_exact(d, k):
+    """fp32 tables (v_mfma_f32_32x32x2_f32 scan): integer-valued scores are
+    exact, so lists AND scores equal the oracle bit for bit, ties included;
+    d=100 runs zero-padded to 128."""
+    rng = np.random.default_rng(7000 + 1000 * d + k)
+    nu, ni = 37 + d, 2000 + 13
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    s, it = ops.score_topk(_f32(U), _f32(I), k)
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, return_scores=True)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy(), ref_s)
+
+
+@pytest.mark.parametrize("d", [64, 100, 128])
+def test_score_topk_fp32_float_faithful(d):
+    """Raw N(0,1) fp32 tables (nn.Embedding's init, not bf16-representable).
+    Scores: within 5e-7 * sum_j |u_j i_j| of the exact (float64) score — an
+    fp32 fmaf chain's error (a numpy emulation of the scan's k order peaks at
+    3.4e-7 over 600K N(0,1) pairs at d = 64..128). Lists: equal to the oracle's (the reference's fp32
+    sum(u * i) loop) except where exact scores are within the fp32 tolerance
+    (tests/topk_checks.py)."""
+    rng = np.random.default_rng(90 + d)
+    nu, ni, k = 150, 5000, 100
+    U = rng.standard_normal((nu, d)).astype(np.float32)
+    I = rng.standard_normal((ni, d)).astype(np.float32)
+    s, it = ops.score_topk(_f32(U), _f32(I), k)
+    s, it = s.cpu().numpy(), it.cpu().numpy().astype(np.int64)
+    S = U.astype(np.float64) @ I.astype(np.float64).T
+    A = np.abs(U.astype(np.float64)) @ np.abs(I.astype(np.float64)).T
+    rows = np.arange(nu)[:, None]
+    assert np.all(np.abs(s - S[rows, it]) <= 5e-7 * A[rows, it])
+    assert np.all(np.diff(s, axis=1) <= 0)
+    ref_i = oracle.recommend_topk(U, I, k)
+    bad = gap_check(it, ref_i, U, I, None, fp32_row_tol(U, I))
+    assert bad <= nu // 16
+
+
+def test_score_topk_fp32_vs_bf16_mode():
+    """bf16-representable fp32 tables: the fp32 scan and the bf16 scan see the
+    same values; integer-valued ones give identical lists and scores."""
+    rng = np.random.default_rng(44)
+    U, I = _int_table(rng, 300, 128), _int_table(rng, 7000, 128)
+    s32, i32 = ops.score_topk(_f32(U), _f32(I), 50)
+    s16, i16 = ops.score_topk(_bf16(U), _bf16(I), 50)
+    assert torch.equal(i32, i16) and torch.equal(s32, s16)
+
+
+# --------------------------------------------------------------------------- k = 1000 (config 5's candidate lists)
+def _excl(rng, U, I, nu, ni, n_max=300):
+    frozen = [rng.choice(ni, size=rng.integers(0, n_max), replace=False) for _ in range(nu)]
+    for u in range(0, nu, 3):  # the best items excluded: the worst case for the thresholds
+        best = np.argsort(-(I @ U[u]), kind="stable")[:40]
+        frozen[u] = np.union1d(frozen[u], best)
+    return frozen
+
+
+@pytest.mark.parametrize("d,k", [(64, 1000), (128, 1000), (128, 1024)])
+def test_score_topk_k1000_guess_exclusion_exact(d, k):
+    """k = 1000 / 1024 (CAP 2048 candidate buffers, 32-key-per-lane finalize
+    sort) over a 2^18+-row catalog, so the guessed-threshold path runs, with
+    exclusions: lists and scores equal the oracle (integer tables, exact
+    scores, massive ties)."""
+    rng = np.random.default_rng(d + k)
+    nu, ni = 24, (1 << 18) + 999
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    frozen = _excl(rng, U, I, nu, ni)
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    s, it = ops.score_topk(_bf16(U), _bf16(I), k,
+                           exclude=(torch.from_numpy(rowptr).to(DEV), torch.from_numpy(cols).to(DEV)))
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, frozen=frozen, return_scores=True)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy(), ref_s)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_score_topk_k1000_many_users_exact(dtype):
+    """k = 1000 over more users than one workgroup holds, short catalog (no
+    guess): fp32 and bf16 scans, exclusion of the best items."""
+    rng = np.random.default_rng(1000)
+    d, nu, ni, k = 64, 2100, 3000, 1000
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    frozen = _excl(rng, U, I, nu, ni, n_max=100)
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    t = _f32 if dtype == "f32" else _bf16
+    s, it = ops.score_topk(t(U), t(I), k,
+                           exclude=(torch.from_numpy(rowptr).to(DEV), torch.from_numpy(cols).to(DEV)))
+    sel = np.arange(0, nu, 7)  # an oracle sample of the users (the per-user loop is slow)
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, users=sel, frozen=[frozen[u] for u in sel],
+                                         return_scores=True)
+    assert np.array_equal(it.cpu().numpy()[sel].astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy()[sel], ref_s)
+
+
+def test_score_topk_sharded_k1000_equals_single_pass():
+    """Config 5's candidate lists from an item-sharded catalog: 8 row shards
+    (global ids through item_base), each a top-1000, merged by the streaming
+    merge (8 x 1000 > 2048 entries) — bit-identical to one pass."""
+    rng = np.random.default_rng(808)
+    d, nu, ni, k = 128, 300, 40000, 1000
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    Ub, Ib = _bf16(U), _bf16(I)
+    full_s, full_i = ops.score_topk(Ub, Ib, k)
+    bounds = np.linspace(0, ni, 9).astype(int)
+    parts = [ops.score_topk(Ub, Ib[lo:hi], k, item_base=int(lo))
+             for lo, hi in zip(bounds[:-1], bounds[1:])]
+    ms, mi = ops.topk_merge(torch.stack([p[0] for p in parts]), torch.stack([p[1] for p in parts]), k)
+    assert torch.equal(mi, full_i) and torch.equal(ms, full_s)
+
+
+def test_topk_merge_streaming_matches_oracle():
+    """parts * k_in > 2048 entries per user (8 x 1000): the streaming merge
+    kernel, with empty slots, against the oracle."""
+    rng = np.random.default_rng(14)
+    P, n, k_in, k_out = 8, 37, 1000, 1000
+    sc = rng.integers(-50, 50, size=(P, n, k_in)).astype(np.float32)
+    items = np.stack([rng.permutation(200000)[: n * k_in].reshape(n, k_in)
+                      for _ in range(P)]).astype(np.int32)
+    for p in range(P):
+        for u in range(n):
+            o = np.lexsort((items[p, u], -sc[p, u]))
+            sc[p, u], items[p, u] = sc[p, u][o], items[p, u][o]
+    items[2, 5, 600:] = -1
+    sc[2, 5, 600:] = -np.inf
+    items[:, 7, 10:] = -1  # a user with only 80 entries: the tail must be empty
+    sc[:, 7, 10:] = -np.inf
+    ms, mi = ops.topk_merge(torch.from_numpy(sc).to(DEV), torch.from_numpy(items).to(DEV), k_out)
+    rs, ri = oracle.topk_merge(sc, items, k_out)
+    assert np.array_equal(mi.cpu().numpy().astype(np.int64), ri)
+    assert np.array_equal(ms.cpu().numpy(), rs)
 
 
 def test_topk_merge_matches_oracle():

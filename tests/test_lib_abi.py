@@ -42,14 +42,25 @@ def test_version_and_error_string():
 def test_argument_errors_without_gpu():
     lib = _backend.load_library()
     # k out of range -> DR_EINVAL with a message; nothing touches the device
-    rc = lib.dr_score_topk(None, None, 10, None, 10, 0, 64, 0, None, None, None, None, None, 0, None)
+    bf16, f32 = _backend.DR_BF16, _backend.DR_F32
+    rc = lib.dr_score_topk(None, None, 10, None, 10, 0, bf16, 64, 0, None, None, None, None, None,
+                           0, None)
     assert rc == -1 and b"k must be" in lib.dr_last_error()
-    rc = lib.dr_score_topk(None, None, 10, None, 10, 0, 48, 10, None, None, None, None, None, 0, None)
+    rc = lib.dr_score_topk(None, None, 10, None, 10, 0, bf16, 48, 10, None, None, None, None, None,
+                           0, None)
     assert rc == -1 and b"d must be" in lib.dr_last_error()
+    rc = lib.dr_score_topk(None, None, 10, None, 10, 0, f32, 512, 10, None, None, None, None, None,
+                           0, None)
+    assert rc == -1 and b"fp32 d must be" in lib.dr_last_error()
+    rc = lib.dr_score_topk(None, None, 10, None, 10, 0, _backend.DR_I32, 64, 10, None, None, None,
+                           None, None, 0, None)
+    assert rc == -1 and b"DR_BF16 or DR_F32" in lib.dr_last_error()
     rc = lib.dr_ild_embedding(None, 3, 5, 500, None, 10, 128, 0, None, None)
     assert rc == -1
+    rc = lib.dr_topk_merge(None, None, 3, 10, 1000, 2000, None, None, None)
+    assert rc == -1 and b"k_out must be <= 1024" in lib.dr_last_error()
     rc = lib.dr_topk_merge(None, None, 3, 10, 1000, 10, None, None, None)
-    assert rc == -1
+    assert rc == -1 and b"null pointer" in lib.dr_last_error()  # 3 x 1000 > 2048 is accepted
     rc = lib.dr_mmr_rerank(None, None, 4, 2000, None, 10, 128, 10, 0.5, None, None)
     assert rc == -1 and b"C must be" in lib.dr_last_error()
     # empty inputs are a no-op success
@@ -58,10 +69,29 @@ def test_argument_errors_without_gpu():
 
 def test_workspace_query_is_host_only():
     lib = _backend.load_library()
-    ws = lib.dr_score_topk_workspace(1_000_000, 10_000_000, 128, 100)
+    bf16, f32 = _backend.DR_BF16, _backend.DR_F32
+    ws = lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100)
     # candidate buffers: n_users_pad * CAP(512) * 8 B for the single chunk, + counts
     assert ws >= 1_000_000 * 512 * 8
-    assert lib.dr_score_topk_workspace(10, 10, 48, 10) == 0  # unsupported d
+    assert lib.dr_score_topk_workspace(10, 10, bf16, 48, 10) == 0  # unsupported d
+    assert lib.dr_score_topk_workspace(10, 10, f32, 512, 10) == 0  # no fp32 instance at 512
+    # fp32 rows are twice as wide: same geometry as bf16 at 2d (k=1000 needs CAP 2048)
+    assert lib.dr_score_topk_workspace(4096, 2000, f32, 64, 1000) == \
+        lib.dr_score_topk_workspace(4096, 2000, bf16, 128, 1000)
+    assert lib.dr_score_topk_workspace(4096, 2000, bf16, 128, 1000) >= 4096 * 2048 * 8
+
+
+def test_score_widths_and_padding_host_logic():
+    assert ops.score_width(torch.float32, 100) == 128
+    assert ops.score_width(torch.bfloat16, 100) == 128
+    assert ops.score_width(torch.bfloat16, 300) == 512
+    assert ops.score_width(torch.float32, 16) == 32
+    with pytest.raises(ValueError):
+        ops.score_width(torch.float32, 300)
+    t = torch.arange(6, dtype=torch.float32).reshape(2, 3)
+    p = ops.pad_columns(t, 8)
+    assert p.shape == (2, 8) and torch.equal(p[:, :3], t) and not p[:, 3:].any()
+    assert ops.pad_columns(t, 3) is t
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")

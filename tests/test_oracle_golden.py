@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import oracle
+from topk_checks import fp32_row_tol, gap_check
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -38,6 +39,23 @@ def test_recommendations(name):
     U, I, k = g["U"], g["I"], int(g["k"])
     recs = oracle.recommend_topk(U, I, k, frozen=_frozen(g["train"], U.shape[0]))
     assert np.array_equal(recs, g["recs"])
+
+
+@pytest.mark.parametrize("name", ["recs_fp32_d100_k10", "recs_fp32_d100_k100",
+                                  "recs_fp32_d100_k1000", "ml100k_d100"])
+def test_recommendations_raw_fp32(name):
+    """Raw N(0,1) fp32 tables at d=100: the oracle's fp32 sums (numpy order)
+    against the reference's (torch order) — equal except at near-ties."""
+    g = load(name)
+    U, I = g["U"], g["I"]
+    k = int(g["k"]) if "k" in g.files else 10
+    frozen = _frozen(g["train"], U.shape[0])
+    recs = oracle.recommend_topk(U, I, k, frozen=frozen)
+    bad = gap_check(recs, g["recs"], U, I, oracle.exclusion_csr(frozen), fp32_row_tol(U, I))
+    assert bad <= max(1, U.shape[0] // 64)
+    if name == "ml100k_d100":
+        ild = oracle.ild_embedding_f64(g["recs"], I, "cosine")
+        assert np.allclose(ild, g["ild"], rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("k", [1, 2, 10, 100])
@@ -87,6 +105,20 @@ def test_ml100k_cfg1_recs_and_ild():
     ild = oracle.ild_embedding_f64(g["recs"], I, "cosine")
     assert np.allclose(ild, g["ild"], rtol=1e-5, atol=1e-6)
     del En
+
+
+def test_topk_merge_equals_single_pass_k1000():
+    rng = np.random.default_rng(3)
+    U = rng.integers(-2, 3, size=(6, 16)).astype(np.float32)
+    I = rng.integers(-2, 3, size=(5000, 16)).astype(np.float32)
+    full_i, full_s = oracle.recommend_topk(U, I, 1000, return_scores=True)
+    bounds = np.linspace(0, 5000, 9).astype(int)
+    parts = [oracle.recommend_topk(U, I[lo:hi], 1000, return_scores=True)
+             for lo, hi in zip(bounds[:-1], bounds[1:])]
+    ms, mi = oracle.topk_merge(np.stack([p[1] for p in parts]),
+                               np.stack([p[0] + lo for p, lo in zip(parts, bounds)]), 1000)
+    assert np.array_equal(mi, full_i)
+    assert np.array_equal(ms, full_s)
 
 
 def test_topk_merge_equals_single_pass():

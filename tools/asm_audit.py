@@ -2,7 +2,7 @@
 
     python tools/asm_audit.py [-D KEY=VAL ...]
 
-Compiles csrc/score_topk.hip to gfx950 assembly with the given defines and, for
+Compiles csrc/score_scan_bf16.hip and score_scan_f32.hip to gfx950 assembly with the given defines and, for
 every score_scan_kernel instantiation, prints the VGPR count, the scratch
 bytes per lane, and the scratch instructions and `s_waitcnt vmcnt(0)` found
 between the kernel's first and last MFMA (the hot loop). Any scratch access in
@@ -23,19 +23,25 @@ def main():
     ap.add_argument("-D", dest="defines", action="append", default=[])
     ap.add_argument("--filter", default="score_scan_kernel")
     args = ap.parse_args()
-    out = "/tmp/score_topk_audit.s"
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-           "-munsafe-fp-atomics", f"-I{ROOT}/include", f"-I{PKG}/csrc", "--cuda-device-only",
-           "-S", f"{PKG}/csrc/score_topk.hip", "-o", out] + [f"-D{d}" for d in args.defines]
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        print(r.stderr)
-        return 1
-    text = open(out).read()
+    bad = 0
+    for src in ("score_scan_bf16", "score_scan_f32"):
+        out = f"/tmp/{src}_audit.s"
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+               "-munsafe-fp-atomics", f"-I{ROOT}/include", f"-I{PKG}/csrc", "--cuda-device-only",
+               "-S", f"{PKG}/csrc/{src}.hip", "-o", out] + [f"-D{d}" for d in args.defines]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            print(r.stderr)
+            return 1
+        bad += audit(open(out).read(), args.filter)
+    return 0 if bad == 0 else 2
+
+
+def audit(text, filt):
     starts = [(m.start(), m.group(1)) for m in re.finditer(r"^(_Z\S+):", text, re.M)]
     bad = 0
     for i, (pos, name) in enumerate(starts):
-        if args.filter not in name:
+        if filt not in name:
             continue
         end = starts[i + 1][0] if i + 1 < len(starts) else len(text)
         body = text[pos:end]
@@ -49,11 +55,11 @@ def main():
         vg = re.search(r"\.amdhsa_next_free_vgpr (\d+)", meta.group(1)).group(1) if meta else "?"
         sc = re.search(r"\.amdhsa_private_segment_fixed_size (\d+)",
                        meta.group(1)).group(1) if meta else "?"
-        short = re.sub(r"_ZN12_GLOBAL__N_1\d+", "", name)[:60]
+        short = re.sub(r"_ZN7dr_topk\d+", "", name)[:60]
         print(f"{short:60s} vgpr={vg:>4} scratch={sc:>4} mfma={len(mf):3d} "
               f"scratch_loads={scr:3d} vmcnt0={w0}")
         bad += scr
-    return 0 if bad == 0 else 2
+    return bad
 
 
 if __name__ == "__main__":

@@ -38,7 +38,7 @@ def main():
     U = (torch.randn(args.users, args.dim, generator=g, device=dev) / args.dim ** 0.5).to(torch.bfloat16)
     I = (torch.randn(args.items, args.dim, generator=g, device=dev) / args.dim ** 0.5).to(torch.bfloat16)
     L = B.lib()
-    ws_bytes = L.dr_score_topk_workspace(args.users, args.items, args.dim, args.k)
+    ws_bytes = L.dr_score_topk_workspace(args.users, args.items, B.DR_BF16, args.dim, args.k)
     out_s = torch.empty(args.users, args.k, device=dev)
     out_i = torch.empty(args.users, args.k, dtype=torch.int32, device=dev)
     res = {}
@@ -46,7 +46,8 @@ def main():
         ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-        rc = L.dr_score_topk(U.data_ptr(), None, args.users, I.data_ptr(), args.items, 0, args.dim,
+        rc = L.dr_score_topk(U.data_ptr(), None, args.users, I.data_ptr(), args.items, 0,
+                             B.DR_BF16, args.dim,
                              args.k, None, None, out_s.data_ptr(), out_i.data_ptr(), ws.data_ptr(),
                              ws_bytes, B.stream(dev))
         ev1.record()
@@ -56,9 +57,10 @@ def main():
     import ctypes
     fn = L.dr_score_topk_diag_offset
     fn.restype = ctypes.c_size_t
-    fn.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    fn.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_void_p]
     grid = ctypes.c_int(0)
-    off = fn(args.users, args.items, args.dim, args.k, ctypes.byref(grid))
+    off = fn(args.users, args.items, B.DR_BF16, args.dim, args.k, ctypes.byref(grid))
     # the kernel aligns the workspace base up to 256 B
     base = (-ws.data_ptr()) % 256
     blk = ws[base + off: base + off + grid.value * 8 * 16 * 8].view(torch.int64).cpu()

@@ -59,13 +59,14 @@ def main():
 
     def run(t):
         L = libs[t]
-        ws_bytes = L.dr_score_topk_workspace(args.users, args.items, d, args.k)
+        ws_bytes = L.dr_score_topk_workspace(args.users, args.items, B.DR_BF16, d, args.k)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         s = torch.empty(args.users, args.k, device=dev)
         i = torch.empty(args.users, args.k, dtype=torch.int32, device=dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        rc = L.dr_score_topk(U.data_ptr(), None, args.users, I.data_ptr(), args.items, 0, d,
+        rc = L.dr_score_topk(U.data_ptr(), None, args.users, I.data_ptr(), args.items, 0,
+                             B.DR_BF16, d,
                              args.k, None, None, s.data_ptr(), i.data_ptr(), ws.data_ptr(),
                              ws_bytes, stream)
         e1.record()
