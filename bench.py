@@ -11,7 +11,9 @@ One step = one pass of the hot path over the whole synthetic workload:
   ILD of the final top-k lists of this rank's users.
 Ranks form a (N/S) x S grid (divrec.distributed.grid_layout): the S ranks of
 a row row-shard the item table contiguously and share one user slice. S =
---item-shards (auto: 2 for even N; `--item-shards N` is pure item sharding).
+--item-shards (default N: pure 8-way item row-sharding at N=8, the north-star
+layout). At N >= 4 the (N/2) x 2 grid is timed too and reported beside the
+line as `grid_alt` (fewer, longer item shards: less survivor work per rank).
 Inputs are resident in HBM before timing (the item table is also replicated
 for the ILD gathers); the total work is fixed, so scaling is "strong".
 value = U*I / step time (max over ranks).
@@ -20,15 +22,19 @@ Rank 0 prints ONE JSON line. The `roofline` object is for the dominant kernel
 (score_topk: bound = MFMA, achieved = 2*U*I_shard*d flop / average HIP-event
 time of the call on its stream); `traffic` comes from a committed rocprofv3 PMC
 summary (profiles/pmc_traffic.json) when one exists for this exact config.
-`cpu_baseline` (N=1 only) times the CPU oracle — the reference algorithm,
-restated — on a bounded user sample on this host.
+`cpu_baseline` (N=1 only) times the reference's per-user loop restated in
+torch (oracle.reference_loop_topk: set difference, torch.full, embedding
+gather + sum(u*i), argsort, slice) on all of this host's CPU share, on a
+bounded user sample, with the vectorised torch GEMM + topk beside it.
 
 Secondary workloads (single GPU, one JSON line each, same schema; the driver
 runs the default only): ``--workload score1m`` (BASELINE configs[1]: 1M x 1M,
 d=64, top-100), ``gather`` (the MatrixFactorization.forward row gather on
 1M x 1M fp32 tables, HBM roofline), ``bpr`` (configs[2]: one BPR training step
 = fused gather + loss + gradient scatter + dense Adam over both tables) and
-``mmr`` (configs[4]: MMR re-rank of 1000 candidates to 100 per user).
+``mmr`` (configs[4]: the top-1000 scan of the 10M-item catalog, MMR re-rank
+of those 1000 candidates to 100 per user, and the ILD of the re-ranked lists;
+users sharded over the ranks under torchrun, one all_reduce for the mean ILD).
 """
 from __future__ import annotations
 
@@ -45,7 +51,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from divrec import ops  # noqa: E402
-from divrec.distributed import exchange_partials, grid_layout, shard_range  # noqa: E402
+from divrec.distributed import (exchange_partials, global_mean, grid_layout,  # noqa: E402
+                                shard_range)
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
@@ -65,8 +72,10 @@ def parse():
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--item-shards", type=int, default=0,
-                    help="ranks that row-shard the item table per user slice (0 = auto: "
-                         "2 for an even world size, else the world size)")
+                    help="ranks that row-shard the item table per user slice (0 = the world "
+                         "size: pure item sharding)")
+    ap.add_argument("--no-alt-grid", action="store_true",
+                    help="skip timing the (N/2) x 2 grid beside the main layout (N >= 4)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (gloo: multi-rank rehearsal on one GPU)")
     ap.add_argument("--same-device", action="store_true",
@@ -76,6 +85,9 @@ def parse():
                          "over the whole catalog on one device and require identical lists")
     ap.add_argument("--workload", default="catalog",
                     choices=["catalog", "score1m", "gather", "bpr", "mmr"])
+    ap.add_argument("--candidates", type=int, default=1000, help="mmr: top-C candidates per user")
+    ap.add_argument("--mmr-k", type=int, default=100, help="mmr: re-ranked list length")
+    ap.add_argument("--mmr-lambda", type=float, default=0.5)
     return ap.parse_args()
 
 
@@ -91,46 +103,67 @@ def gen_table(rows: int, d: int, seed: int, device, block: int = 1 << 20) -> tor
     return out
 
 
-def cpu_baseline(U: torch.Tensor, I: torch.Tensor, recs: torch.Tensor, k: int, budget_s: float):
-    """Time the CPU oracle (reference algorithm restated) on a bounded sample."""
-    sys.path.insert(0, ROOT)
-    import numpy as np
+def host_cpu():
+    """(threads used, visible logical CPUs, CPU model) of this host. The
+    threads are this process's CPU share (OMP_NUM_THREADS, 16 on the GPU box,
+    whose os.cpu_count() shows the whole machine), at most os.cpu_count()."""
+    visible = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", visible) or visible)
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return max(1, min(share, visible)), visible, model
 
+
+def cpu_baseline(U: torch.Tensor, I: torch.Tensor, recs: torch.Tensor, k: int, budget_s: float):
+    """The reference's per-user scoring loop, restated in torch with the same
+    ops (oracle.reference_loop_topk), timed on this host's CPU share over a
+    bounded user sample; the vectorised CPU form and the ILD loop beside it."""
+    sys.path.insert(0, ROOT)
     import oracle
 
-    Uh = U[:64].float().cpu().numpy()
-    Ih = I.float().cpu().numpy()
+    threads, visible, model = host_cpu()
+    torch.set_num_threads(threads)
+    Uh = U[:64].float().cpu()
+    Ih = I.float().cpu()
     n_items = Ih.shape[0]
-    # scoring + top-k: per-user loop of the reference (fp32 products, sum, full sort)
     t0 = time.perf_counter()
-    oracle.recommend_topk(Uh, Ih, k, users=[0])
+    oracle.reference_loop_topk(Uh, Ih, k, users=[0])
     per_user = time.perf_counter() - t0
     n_users = int(max(1, min(16, budget_s * 0.8 // max(per_user, 1e-3))))
     t0 = time.perf_counter()
-    oracle.recommend_topk(Uh, Ih, k, users=list(range(1, 1 + n_users)))
+    oracle.reference_loop_topk(Uh, Ih, k, users=list(range(1, 1 + n_users)))
     dt = time.perf_counter() - t0
     pairs_per_s = n_users * n_items / dt
     # vectorised CPU (SURVEY.md §8d (ii)): torch fp32 block GEMM + topk, all threads
     n_vec = 64
-    Ut = torch.from_numpy(Uh[:n_vec])
-    It = torch.from_numpy(Ih)
     t0 = time.perf_counter()
-    torch.topk(Ut @ It.T, k, dim=1)
+    torch.topk(Uh[:n_vec] @ Ih.T, k, dim=1)
     vec_dt = time.perf_counter() - t0
     # ILD (cosine, from embeddings): per-user pairwise sum of the reference formula
     rh = recs[:2000].long().cpu().numpy()
+    Ihn = Ih.numpy()
     t0 = time.perf_counter()
-    oracle.ild_embedding_f64(rh, Ih, "cosine")
+    oracle.ild_embedding_f64(rh, Ihn, "cosine")
     ild_dt = time.perf_counter() - t0
     return {
         "value": pairs_per_s,
         "unit": "scored pairs/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"oracle.recommend_topk (reference get_model_recommendations loop: fp32 "
-                  f"sum(u*i) + full stable argsort) for {n_users} users x {n_items} items in "
-                  f"{dt:.1f}s; ILD: oracle.ild_embedding_f64 on {len(rh)} users "
-                  f"-> {len(rh) / ild_dt:.0f} users/s",
+        "cpu_model": model,
+        "cpus_visible": visible,
+        "sample": f"oracle.reference_loop_topk (the reference get_model_recommendations loop "
+                  f"restated in torch: frozenset difference, LongTensor, torch.full, embedding "
+                  f"gather + sum(u*i), argsort, slice, tolist) for {n_users} users x {n_items} "
+                  f"items in {dt:.1f}s on {threads} threads; ILD: oracle.ild_embedding_f64 on "
+                  f"{len(rh)} users -> {len(rh) / ild_dt:.0f} users/s (1 thread)",
         "ild_users_per_s": len(rh) / ild_dt,
         "vectorized": {"value": n_vec * n_items / vec_dt, "unit": "scored pairs/s",
                        "cores": torch.get_num_threads(),
@@ -231,27 +264,11 @@ def load_traffic(cfg_key: str):
     return None
 
 
-def main():
-    args = parse()
-    if args.workload != "catalog":
-        return secondary(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    dev_index = 0 if args.same_device else local_rank
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
-    S = 1
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-        S = args.item_shards or (2 if world % 2 == 0 else world)
+def time_layout(args, world: int, dev, S: int, record_recs: bool = True):
+    """Time the catalog step on a (world/S) x S grid of ranks: warmup, barrier,
+    exactly args.steps timed steps, barrier; max over ranks. Returns a dict
+    with the step time, per-kernel HIP-event times and this rank's data."""
     lay = grid_layout(S) if world > 1 else None
-
     U_n, I_n, d, k = args.users, args.items, args.dim, args.k
     # (user slice) x (item shard) of this rank in the grid; the item table is
     # also replicated in full for the ILD gathers
@@ -261,7 +278,6 @@ def main():
     items = gen_table(I_n, d, 2, dev)
     shard = items[lo:hi]
     torch.cuda.synchronize()
-
     ev = {n: [] for n in ("topk0", "topk1", "ild0", "ild1")}
 
     def step(record: bool):
@@ -297,16 +313,44 @@ def main():
     dt = time.perf_counter() - t0
     topk_s = sum(a.elapsed_time(b) for a, b in zip(ev["topk0"], ev["topk1"])) / 1e3 / args.steps
     ild_s = sum(a.elapsed_time(b) for a, b in zip(ev["ild0"], ev["ild1"])) / 1e3 / args.steps
-    t = torch.tensor([dt, ild_s], dtype=torch.float64,
+    t = torch.tensor([dt, ild_s, topk_s], dtype=torch.float64,
                      device="cpu" if args.backend == "gloo" else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt, ild_max = float(t[0]), float(t[1])
-    step_s = dt / args.steps
+    return {"lay": lay, "S": S, "dt": float(t[0]), "ild_max": float(t[1]),
+            "topk_max": float(t[2]), "topk_s": topk_s, "users": users, "items": items,
+            "recs": recs if record_recs else None, "u_lo": u_lo, "u_hi": u_hi, "lo": lo, "hi": hi}
+
+
+def main():
+    args = parse()
+    if args.workload == "mmr":
+        return mmr_pipeline(args)
+    if args.workload != "catalog":
+        return secondary(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    dev_index = 0 if args.same_device else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    S = 1
+    if world > 1:
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        S = args.item_shards or world
+    r = time_layout(args, world, dev, S)
+    U_n, I_n, d, k = args.users, args.items, args.dim, args.k
+    step_s = r["dt"] / args.steps
+    u_lo, u_hi, lo, hi = r["u_lo"], r["u_hi"], r["lo"], r["hi"]
 
     cfg_key = f"U{U_n}_I{I_n}_d{d}_k{k}_G{world}"
     flops = 2.0 * (u_hi - u_lo) * (hi - lo) * d
-    achieved = flops / topk_s / 1e12
+    achieved = flops / r["topk_s"] / 1e12
     traffic = load_traffic(cfg_key)
     result = {
         "metric": "scored pairs/sec + ILD-eval users/sec, 1M x 10M d=128 at 1/2/4/8 GPU",
@@ -330,9 +374,10 @@ def main():
                            + (f" x user-shard{world // S}" if world // S > 1 else ""),
             "item_shards": S,
         },
-        "ild_users_per_s": U_n / ild_max,
-        "score_topk_ms": topk_s * 1e3,
-        "ild_ms": ild_max * 1e3,
+        "ild_users_per_s": U_n / r["ild_max"],
+        "score_topk_ms": r["topk_s"] * 1e3,
+        "score_topk_ms_max_over_ranks": r["topk_max"] * 1e3,
+        "ild_ms": r["ild_max"] * 1e3,
         "roofline": {
             "bound": "mfma",
             "achieved": achieved,
@@ -346,11 +391,28 @@ def main():
         "cpu_baseline": None,
     }
     if args.check_users > 0:
-        result["check"] = check_lists(args, lay, users, items, recs, u_lo, U_n, k, world)
+        result["check"] = check_lists(args, r["lay"], r["users"], r["items"], r["recs"], u_lo,
+                                      U_n, k, world)
+    if world >= 4 and world % 2 == 0 and S != 2 and not args.no_alt_grid:
+        # the (N/2) x 2 grid beside the main layout: same work,
+        # 2-way item shards, users split N/2 ways
+        del r
+        torch.cuda.empty_cache()
+        a = time_layout(args, world, dev, 2, record_recs=False)
+        a_step = a["dt"] / args.steps
+        result["grid_alt"] = {
+            "layout": f"{world // 2} x 2 grid (item rows sharded 2 ways, users {world // 2} ways, "
+                      f"all_to_all inside each pair)",
+            "item_shards": 2, "value": U_n * I_n / a_step, "unit": "scored pairs/s",
+            "ms_per_step": a_step * 1e3, "score_topk_ms": a["topk_s"] * 1e3,
+            "roofline_frac": 2.0 * (a["u_hi"] - a["u_lo"]) * (a["hi"] - a["lo"]) * d
+                             / a["topk_s"] / 1e12 / MFMA_BF16_PEAK_TFLOPS}
+        r = None
     if rank == 0:
         with_measured(result["roofline"], dev, "mfma_bf16_tflops")
     if world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(users, items, recs, k, args.cpu_budget_s)
+        result["cpu_baseline"] = cpu_baseline(r["users"], r["items"], r["recs"], k,
+                                              args.cpu_budget_s)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -621,33 +683,113 @@ def secondary(args):
                                    "frac": 3 * d * 4 * B / tb / 1e9 / ATOMIC_F32_GBS})
         return 0
 
-    if args.workload == "mmr":
-        U_n, I_n, d, C, kout, lam = 1_000_000, 10_000_000, 128, 1000, 100, 0.5
-        items = gen_table(I_n, d, 2, dev)
-        cand = torch.randint(0, I_n, (U_n, C), generator=g, device=dev, dtype=torch.int32)
-        sc = torch.sort(torch.rand(U_n, C, generator=g, device=dev), dim=1, descending=True).values
-        wall, dt = _timed(lambda: ops.mmr_rerank(cand, sc, items, kout, lam), args.steps,
-                          args.warmup)
-        per_user = C * d * 2 + C * 8 + kout * 4
-        cpu = None
-        if want_cpu:
-            import oracle
-
-            m = 4
-            Eh = items.float().cpu().numpy()
-            t0 = time.perf_counter()
-            oracle.mmr_greedy(cand[:m].cpu().numpy(), sc[:m].cpu().numpy(), Eh, kout, lam)
-            t = time.perf_counter() - t0
-            cpu = {"value": m / t, "unit": "users/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle.mmr_greedy (float64 numpy), {m} users, {t:.2f}s"}
-        _line("MMR re-rank users/sec, top-1000 -> top-100, d=128 (BASELINE configs[4])",
-              U_n / wall, "users/s", args, wall, "bf16",
-              {"workload": f"dr_mmr_rerank: {U_n} users x {C} candidates -> {kout}, "
-                           f"lambda={lam}, item table {I_n}x{d} bf16", "users": U_n, "dim": d},
-              dict(_hbm(per_user * U_n, dt), kernel="dr_mmr_rerank",
-                   per_unit=f"{per_user} B/user"), cpu)
-        return 0
     raise ValueError(args.workload)
+
+
+def mmr_pipeline(args):
+    """configs[4]: per user the top-C candidates of the 10M-item catalog
+    (dr_score_topk, k = C), the MMR re-rank of those C to k_out (dr_mmr_rerank)
+    and the cosine ILD of the re-ranked lists (dr_ild_embedding). Users are
+    sharded over the ranks (torchrun), the item table is replicated; the only
+    collective is the all_reduce of the ILD (sum, count). value = users/s of
+    the whole pipeline (max over ranks); the three kernels are timed apart."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dev_index = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    if world > 1:
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    U_n, I_n, d = args.users, args.items, args.dim
+    C, kout, lam = args.candidates, args.mmr_k, args.mmr_lambda
+    u_lo, u_hi = shard_range(U_n, world, rank)
+    users = gen_table(U_n, d, 1, dev)[u_lo:u_hi].contiguous()
+    items = gen_table(I_n, d, 2, dev)
+    torch.cuda.synchronize()
+    ev = []
+    out = {}
+
+    def step(record):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        if e:
+            e[0].record()
+        sc, cand = ops.score_topk(users, items, C)
+        if e:
+            e[1].record()
+        picks = ops.mmr_rerank(cand, sc, items, kout, lam)
+        if e:
+            e[2].record()
+        ild = ops.ild_embedding(picks, items, "cosine")
+        mean = global_mean(ild) if world > 1 else torch.sum(ild, 0) / ild.numel()
+        if e:
+            e[3].record()
+            ev.append(e)
+        out.update(cand=cand, sc=sc, picks=picks, mean=mean)
+
+    for _ in range(args.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ph = [sum(e[j].elapsed_time(e[j + 1]) for e in ev) / 1e3 / args.steps for j in range(3)]
+    t = torch.tensor([dt] + ph, dtype=torch.float64, device="cpu" if args.backend == "gloo" else dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    step_s = float(t[0]) / args.steps
+    topk_s, mmr_s, ild_s = ph  # this rank's kernels (rank 0 prints)
+    n_r = u_hi - u_lo
+    per_user = C * d * 2 + C * 8 + kout * 4  # candidate rows + (id, score) + picks
+    flops = 2.0 * n_r * I_n * d
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        import oracle
+
+        m = 4
+        Eh = items.float().cpu().numpy()
+        t1 = time.perf_counter()
+        oracle.mmr_greedy(out["cand"][:m].cpu().numpy(), out["sc"][:m].cpu().numpy(), Eh, kout, lam)
+        tm = time.perf_counter() - t1
+        cpu = {"value": m / tm, "unit": "users/s (MMR re-rank only)", "cores": 1, "kind": "port",
+               "sample": f"oracle.mmr_greedy (float64 numpy) on the first {m} users' real "
+                         f"top-{C} lists, {tm:.2f}s"}
+    rec = {"metric": f"MMR pipeline users/sec: top-{C} of {I_n} items -> MMR top-{kout} -> ILD, "
+                     f"d={d} (BASELINE configs[4])",
+           "value": U_n / step_s, "unit": "users/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+           "data": "synthetic (N(0,1/sqrt(d)) bf16 tables, seeded per 1M-row block)",
+           "config": {"workload": f"{U_n} users (sharded {world} ways) x {I_n} items, "
+                                  f"top-{C} scan -> MMR lambda={lam} -> {kout} -> cosine ILD, "
+                                  f"all_reduce of the ILD (sum, count)",
+                      "users": U_n, "items": I_n, "dim": d, "candidates": C, "k": kout,
+                      "parallelism": f"user-shard{world}"},
+           "topk_ms": topk_s * 1e3, "mmr_ms": mmr_s * 1e3, "ild_ms": ild_s * 1e3,
+           "mmr_users_per_s": n_r / mmr_s, "mean_ild": float(out["mean"]),
+           "roofline": {"bound": "mfma", "achieved": flops / topk_s / 1e12,
+                        "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": flops / topk_s / 1e12 / MFMA_BF16_PEAK_TFLOPS, "traffic": None,
+                        "kernel": f"dr_score_topk k={C} (the step's dominant kernel)"},
+           "mmr_roofline": dict(_hbm(per_user * n_r, mmr_s), kernel="dr_mmr_rerank",
+                                per_unit=f"{per_user} B/user"),
+           "cpu_baseline": cpu}
+    if rank == 0:
+        with_measured(rec["roofline"], dev, "mfma_bf16_tflops")
+        with_measured(rec["mmr_roofline"], dev, "hbm_copy_gbs")
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

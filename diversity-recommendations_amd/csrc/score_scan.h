@@ -275,8 +275,132 @@ struct CompactResult {
 // k + kSlack keys remain at or above the bucket's lower bound. The bound's
 // score is the new threshold: >= k kept keys rank above any later item of
 // equal or lower score. Excluded items are dropped first.
+//
+// The buffer is streamed in chunks of 64 * P keys (P per lane) at every level
+// instead of being held in registers, so the function's register footprint is
+// the same for every capacity: a register-resident 2048-key buffer (CAP =
+// 2048, k up to 1024) made the callee clobber so many registers that the
+// caller spilled its B fragments inside the MFMA loop (5x slower tiles).
 template <int P>
-__device__ DR_COMPACT_INLINE CompactResult compact_buffer(uint64_t* __restrict__ buf, int n_in, int k,
+__device__ DR_COMPACT_INLINE CompactResult compact_buffer_chunked(uint64_t* __restrict__ buf, int n_in, int k,
+                                                     const int32_t* __restrict__ ex, int exn,
+                                                     uint32_t* __restrict__ hist) {
+  constexpr int CH = 64 * P;
+  const int lane = dr::lane_id();
+  const int nch = (n_in + CH - 1) / CH;
+  wait_vmcnt<0>();  // this wave's candidate stores have landed
+  auto load = [&](int c, uint64_t (&key)[P]) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int e = c * CH + lane * P + i;
+      key[i] = e < n_in ? __hip_atomic_load(buf + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : 0ull;
+    }
+  };
+  // pass 0: drop excluded items (zeroed in place) and count the live keys
+  int total = 0;
+#pragma unroll 1
+  for (int c = 0; c < nch; ++c) {
+    uint64_t key[P];
+    load(c, key);
+    if (exn > 0) {
+#pragma unroll
+      for (int i = 0; i < P; ++i)
+        if (key[i] != 0ull && sorted_contains(ex, exn, (int32_t)dr::key_item(key[i]))) {
+          key[i] = 0ull;
+          buf[c * CH + lane * P + i] = 0ull;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < P; ++i) total += __popcll(__ballot(key[i] != 0ull));
+  }
+  if (exn > 0) wait_vmcnt<0>();  // the zeroed slots are visible to the passes below
+  uint64_t lo = 1ull;  // keep keys >= lo (key 0 = empty slot)
+  CompactResult res{total, -INFINITY};
+  if (total > k + kSlack) {
+    uint64_t pfx = 0ull;
+    int need = k, above = 0, inb = total;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hist[lane * 4 + j] = 0u;
+      wave_lds_sync();
+#pragma unroll 1
+      for (int c = 0; c < nch; ++c) {
+        uint64_t key[P];
+        load(c, key);
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+          const bool in = key[i] != 0ull &&
+                          (shift == 56 || (key[i] >> (shift + 8)) == (pfx >> (shift + 8)));
+          if (in) atomicAdd(&hist[(uint32_t)(key[i] >> shift) & 255u], 1u);
+        }
+      }
+      wave_lds_sync();
+      uint32_t hv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hv[j] = hist[lane * 4 + j];
+      const uint32_t s4 = hv[0] + hv[1] + hv[2] + hv[3];
+      uint32_t sfx = s4;  // inclusive suffix sum over lanes >= this lane
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) {
+        const uint32_t o = __shfl_down(sfx, m);
+        sfx += (lane + m < 64) ? o : 0u;
+      }
+      // this lane's bins from the top (4l+3 .. 4l): the one holding rank `need`
+      uint32_t cum = sfx - s4;  // keys in bins above 4l+3
+      int fb = -1;
+      uint32_t fexcl = 0, fcnt = 0;
+#pragma unroll
+      for (int j = 3; j >= 0; --j) {
+        const uint32_t nx = cum + hv[j];
+        if (fb < 0 && cum < (uint32_t)need && (uint32_t)need <= nx) {
+          fb = lane * 4 + j;
+          fexcl = cum;
+          fcnt = hv[j];
+        }
+        cum = nx;
+      }
+      const int src = __builtin_ctzll(__ballot(fb >= 0));
+      const int b = __builtin_amdgcn_readlane(fb, src);
+      const int excl = __builtin_amdgcn_readlane((int)fexcl, src);
+      inb = __builtin_amdgcn_readlane((int)fcnt, src);
+      pfx |= (uint64_t)b << shift;
+      need -= excl;
+      above += excl;
+      wave_lds_sync();  // hist is re-zeroed by the next level
+      if (above + inb <= k + kSlack) break;
+    }
+    lo = pfx;
+    res.kept = above + inb;
+    res.thr = dr::key_score(pfx);                // smallest score with the kept prefix
+    if (res.thr != res.thr) res.thr = -INFINITY;  // prefix below -FLT_MAX decodes to NaN
+  }
+  // write the kept keys back densely (order is irrelevant), chunk by chunk: a
+  // chunk is in registers before any of its slots is overwritten, and the
+  // write cursor never passes the start of the next chunk
+  int base = 0;
+#pragma unroll 1
+  for (int c = 0; c < nch; ++c) {
+    uint64_t key[P];
+    load(c, key);
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const bool keep = key[i] >= lo;  // lo >= 1 also drops empty keys
+      const uint64_t bal = __ballot(keep);
+      if (keep) buf[base + lane_prefix(bal)] = key[i];
+      base += __popcll(bal);
+    }
+  }
+  wait_vmcnt<0>();
+  return res;
+}
+
+// The same with the whole buffer (<= 64 * P keys) resident in registers:
+// the CAP = 512 scans (k <= 224), whose footprint this exact code fixes
+// (the chunked form measured slower at d = 64, and letting it keep chunk 0
+// in registers spilled the d = 64 tile loop).
+template <int P>
+__device__ DR_COMPACT_INLINE CompactResult compact_buffer_resident(uint64_t* __restrict__ buf, int n_in, int k,
                                                      const int32_t* __restrict__ ex, int exn,
                                                      uint32_t* __restrict__ hist) {
   const int lane = dr::lane_id();
@@ -431,7 +555,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
   constexpr int SR = G::SR;
   constexpr int UPW = NU_T * 32;      // users per wave
   constexpr int UPWG = UPW * kWaves;  // users per workgroup
-  constexpr int P = CAP / 64;         // keys per lane in a compaction
+  constexpr int P = 8;                // keys per lane per compaction chunk (any CAP)
   constexpr int kRing = G::RING;
   constexpr int kStageBytes = G::STAGE_BYTES;
   constexpr int kLpt = G::LPT;
@@ -575,7 +699,11 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         ex = a.excl_items + e0;
         exn = (int)(e1 - e0);
       }
-      const CompactResult r = compact_buffer<P>(cbase + (size_t)slot * CAP, n_in, a.k, ex, exn, hist);
+      CompactResult r;
+      if constexpr (CAP <= 64 * P)
+        r = compact_buffer_resident<CAP / 64>(cbase + (size_t)slot * CAP, n_in, a.k, ex, exn, hist);
+      else
+        r = compact_buffer_chunked<P>(cbase + (size_t)slot * CAP, n_in, a.k, ex, exn, hist);
       vm_done = vmc;
       if (lane == 0) ucnt[slot] = (uint32_t)r.kept;
       wave_lds_sync();

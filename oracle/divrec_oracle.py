@@ -16,6 +16,7 @@ __all__ = [
     "mf_forward",
     "candidates_for_user",
     "recommend_topk",
+    "reference_loop_topk",
     "topk_order",
     "topk_merge",
     "ild_sequential",
@@ -104,6 +105,30 @@ def recommend_topk(
     if return_scores:
         return recs, np.stack(scs).astype(np.float32) if scs else np.zeros((0, k), np.float32)
     return recs
+
+
+def reference_loop_topk(U, I, k: int, users: Sequence[int], frozen=None):
+    """get_model_recommendations (divrec/train/utils.py:53-77) over
+    RankingDataset (divrec/datasets/base_datasets.py:136-171), restated op for
+    op in torch for the CPU baseline (bench.py): per user the frozenset
+    difference of the catalog, torch.LongTensor of the candidate list,
+    torch.full of the user id, MatrixFactorization.forward (embedding gathers
+    + sum(u * i, dim=1), matrix_factorization.py:26-28), argsort descending and
+    the first k ids as a list. U, I: fp32 torch tables. Intra-op parallel on
+    torch's threads like the reference. Returns LongTensor [len(users), k]."""
+    import torch
+
+    items = frozenset(range(I.shape[0]))
+    recs = []
+    with torch.no_grad():
+        for n, u in enumerate(users):
+            fz = frozenset() if frozen is None else frozenset(frozen[n])
+            negatives = torch.LongTensor(list(items - fz))
+            rep = torch.full((len(negatives),), int(u))
+            scores = torch.sum(torch.nn.functional.embedding(rep, U) *
+                               torch.nn.functional.embedding(negatives, I), dim=1)
+            recs.append(negatives[torch.argsort(scores, descending=True)][:k].tolist())
+    return torch.LongTensor(recs)
 
 
 def topk_merge(scores: np.ndarray, items: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:

@@ -48,8 +48,8 @@ def audit(text, filt):
         lines = body.split("\n")
         mf = [j for j, l in enumerate(lines) if "v_mfma" in l]
         loop = lines[mf[0]:mf[-1] + 1] if mf else []
-        scr = sum(1 for l in body.split("\n") if "scratch_load" in l)
-        w0 = sum(1 for l in body.split("\n") if re.search(r"s_waitcnt\s+vmcnt\(0\)", l))
+        scr = sum(1 for l in loop if "scratch_" in l)  # spills inside the MFMA span
+        w0 = sum(1 for l in loop if re.search(r"s_waitcnt\s+vmcnt\(0\)", l))
         meta = re.search(r"\.amdhsa_kernel " + re.escape(name) + r"(.*?)\.end_amdhsa_kernel",
                          text, re.S)
         vg = re.search(r"\.amdhsa_next_free_vgpr (\d+)", meta.group(1)).group(1) if meta else "?"
@@ -57,7 +57,7 @@ def audit(text, filt):
                        meta.group(1)).group(1) if meta else "?"
         short = re.sub(r"_ZN7dr_topk\d+", "", name)[:60]
         print(f"{short:60s} vgpr={vg:>4} scratch={sc:>4} mfma={len(mf):3d} "
-              f"scratch_loads={scr:3d} vmcnt0={w0}")
+              f"loop_scratch={scr:3d} loop_vmcnt0={w0}")
         bad += scr
     return bad
 

@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU session: parity tests, smoke, bench, rocprofv3 kernel summary.
+# One GPU session: parity tests, smoke, headline bench, rocprofv3 kernel
+# summary of the headline step, and the secondary workload lines.
 # Every GPU step has its own time limit; the first failure ends the script.
 set -e
 mkdir -p gpurun_out
@@ -11,3 +12,4 @@ cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1
 cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python bench.py --workload score1m > gpurun_out/wl_score1m.json 2> gpurun_out/wl_score1m.err
+timeout -k 10 300 python bench.py --workload mmr > gpurun_out/wl_mmr.json 2> gpurun_out/wl_mmr.err

@@ -29,10 +29,26 @@ from divrec import _backend as B  # noqa: E402
 LIBDIR = os.path.join(PKG, "divrec", "_lib")
 
 
+# Tags starting with "abi1" are builds from before dr_score_topk took a table
+# dtype (round 1 ABI: no dtype argument), kept to A/B the current build
+# against the round-start kernels in one process.
+_ABI1 = {"dr_score_topk_workspace": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                                      ctypes.c_int]),
+         "dr_score_topk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p])}
+
+
 def lib_for(tag):
     name = "libdivrec_hip.so" if tag == "product" else f"libdivrec_hip_{tag}.so"
     lib = ctypes.CDLL(os.path.join(LIBDIR, name))
-    for fn, (res, args) in B.SIGNATURES.items():
+    sigs = dict(B.SIGNATURES)
+    if tag.startswith("abi1"):
+        sigs.update(_ABI1)
+    for fn in ("dr_score_topk_workspace", "dr_score_topk", "dr_last_error"):
+        res, args = sigs[fn]
         f = getattr(lib, fn)
         f.restype, f.argtypes = res, args
     return lib
@@ -59,14 +75,15 @@ def main():
 
     def run(t):
         L = libs[t]
-        ws_bytes = L.dr_score_topk_workspace(args.users, args.items, B.DR_BF16, d, args.k)
+        dt = () if t.startswith("abi1") else (B.DR_BF16,)
+        ws_bytes = L.dr_score_topk_workspace(args.users, args.items, *dt, d, args.k)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         s = torch.empty(args.users, args.k, device=dev)
         i = torch.empty(args.users, args.k, dtype=torch.int32, device=dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rc = L.dr_score_topk(U.data_ptr(), None, args.users, I.data_ptr(), args.items, 0,
-                             B.DR_BF16, d,
+                             *dt, d,
                              args.k, None, None, s.data_ptr(), i.data_ptr(), ws.data_ptr(),
                              ws_bytes, stream)
         e1.record()
