@@ -292,7 +292,7 @@ def time_layout(args, world: int, dev, S: int, record_recs: bool = True):
             s, i = ops.topk_merge(ps, pi, k)
         if e:
             e[2].record()
-        ild = ops.ild_embedding(i, items, args.ild_kind)
+        ild = ops.ild_embedding(i, items, args.ild_kind, check=False)
         if e:
             e[3].record()
             ev["topk0"].append(e[0]); ev["topk1"].append(e[1])
@@ -525,7 +525,8 @@ def secondary(args):
         It = torch.randn(I_n, d, generator=g, device=dev)
         uid = torch.randint(0, U_n, (n,), generator=g, device=dev)
         iid = torch.randint(0, I_n, (n,), generator=g, device=dev)
-        wall, dt = _timed(lambda: ops.gather_dot(Ut, It, uid, iid), args.steps, args.warmup)
+        wall, dt = _timed(lambda: ops.gather_dot(Ut, It, uid, iid, check=False), args.steps,
+                          args.warmup)
         per_pair = 2 * d * 4 + 2 * 8 + 4
         cpu = None
         if want_cpu:
@@ -539,6 +540,42 @@ def secondary(args):
             t = time.perf_counter() - t0
             cpu = {"value": m / t, "unit": "pairs/s", "cores": 1, "kind": "port",
                    "sample": f"oracle.mf_forward (numpy gather + fp32 row sum), {m} pairs, {t:.2f}s"}
+        # the reference's own call patterns (runs of equal ids, each row read
+        # once per run): RankingDataset's (full((n,), u), candidates) over the
+        # whole catalog for 8 users, and PairWiseDataset's m x m product
+        # (m = 20, the reference config) as model(u, pos) and model(u, neg)
+        def run_bytes(u_, i_):
+            """ids + outputs + each row once per run of equal user ids (the
+            user row and the run's distinct items: what a kernel that keeps a
+            run's rows must read)."""
+            run = torch.cumsum(torch.cat([torch.ones(1, dtype=torch.int64, device=dev),
+                                          (u_[1:] != u_[:-1]).to(torch.int64)]), 0)
+            n_runs = int(run[-1])
+            n_items_run = torch.unique(run * I_n + i_).numel()
+            return u_.numel() * (2 * 8 + 4) + (n_runs + n_items_run) * d * 4
+        m_s = 20
+        n_mu = n // (m_s * m_s)
+        mu = torch.randint(0, U_n, (n_mu,), generator=g, device=dev)
+        mpos = torch.randint(0, I_n, (n_mu, m_s), generator=g, device=dev)
+        mneg = torch.randint(0, I_n, (n_mu, m_s), generator=g, device=dev)
+        pats = {
+            "full_u_candidates": (torch.arange(8, device=dev).repeat_interleave(I_n),
+                                  torch.arange(I_n, device=dev).repeat(8)),
+            "mxm_model_u_pos": (mu.repeat_interleave(m_s * m_s),
+                                mpos.repeat_interleave(m_s, dim=1).reshape(-1)),
+            "mxm_model_u_neg": (mu.repeat_interleave(m_s * m_s), mneg.repeat(1, m_s).reshape(-1)),
+        }
+        patterns = {}
+        for name, (pu, pi) in pats.items():
+            pw, pdt = _timed(lambda: ops.gather_dot(Ut, It, pu, pi, check=False), args.steps,
+                             args.warmup)
+            nb = run_bytes(pu, pi)
+            patterns[name] = dict(_hbm(nb, pdt), pairs=pu.numel(), pairs_per_s=pu.numel() / pw,
+                                  ms=pdt * 1e3, bytes_per_pair=nb / pu.numel(),
+                                  per_unit="2 ids x 8 B + 4 B out per pair + d x 4 B per "
+                                           "user run for its user row and each distinct item")
+            with_measured(patterns[name], dev, "hbm_copy_gbs")
+        del pats
         # the autograd backward of MatrixFactorization.forward (dense embedding
         # gradients): two row gathers + two rows of fp32 atomic adds per pair
         gU, gI = torch.zeros_like(Ut), torch.zeros_like(It)
@@ -558,7 +595,7 @@ def secondary(args):
                            f"{U_n}x{d} and {I_n}x{d}", "pairs": n, "dim": d},
               dict(_hbm(per_pair * n, dt), kernel="dr_gather_dot",
                    per_unit=f"{per_pair} B/pair = 2 rows x {d} x 4 B + 2 ids x 8 B + 4 B out"),
-              cpu, backward=backward)
+              cpu, backward=backward, patterns=patterns)
         return 0
 
     if args.workload == "bpr":
@@ -582,7 +619,7 @@ def secondary(args):
             gI.zero_()
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record()
-            ops.bpr_fwd_bwd(Ut, It, uid, pid, nid, 1.0 / B, gU, gI)
+            ops.bpr_fwd_bwd(Ut, It, uid, pid, nid, 1.0 / B, gU, gI, check=False)
             e[1].record()
             for p_, g_, (m_, v_) in ((Ut, gU, state[0]), (It, gI, state[1])):
                 ops.adam_dense(p_, g_, m_, v_, 1e-3, 0.9, 0.999, 1e-8, 0.0, step_no[0])
@@ -605,7 +642,7 @@ def secondary(args):
         def lazy_step():
             step_no[0] += 1
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            ops.bpr_fwd_bwd(Ut, It, uid, pid, nid, 1.0 / B, gU, gI)
+            ops.bpr_fwd_bwd(Ut, It, uid, pid, nid, 1.0 / B, gU, gI, check=False)
             e[0].record()
             ru, ri = torch.unique(uid), torch.unique(torch.cat([pid, nid]))
             e[1].record()
@@ -722,7 +759,7 @@ def mmr_pipeline(args):
         picks = ops.mmr_rerank(cand, sc, items, kout, lam)
         if e:
             e[2].record()
-        ild = ops.ild_embedding(picks, items, "cosine")
+        ild = ops.ild_embedding(picks, items, "cosine", check=False)
         mean = global_mean(ild) if world > 1 else torch.sum(ild, 0) / ild.numel()
         if e:
             e[3].record()

@@ -11,7 +11,8 @@
 // then covers two contiguous 128-B row segments, the shape at which
 // global_atomic_add_f32 runs at its full rate (MI355X_MICROARCH.md, Global
 // float atomics); 16-B-per-lane chunks would scatter each atomic instruction
-// over 16-B strides. Any d <= 512.
+// over 16-B strides. Any d <= 512. Out-of-range ids are range-checked
+// (include/divrec_hip.h): such a triple reads and adds nothing.
 #include <cmath>
 
 #include "common.h"
@@ -33,17 +34,29 @@ __device__ __forceinline__ float neg_log_sigmoid_grad(float x) {
   return -(x >= 0.f ? e / (1.f + e) : 1.f / (1.f + e));
 }
 
+__device__ __forceinline__ bool in_rows(int64_t r, int64_t n) { return r >= 0 && r < n; }
+
 template <int E>  // row elements per lane: ceil(d / 32)
 __global__ __launch_bounds__(kBlock) void bpr_kernel(
-    const float* __restrict__ U, const float* __restrict__ I, int64_t d,
+    const float* __restrict__ U, int64_t nu, const float* __restrict__ I, int64_t ni, int64_t d,
     const int64_t* __restrict__ uid, const int64_t* __restrict__ pid,
     const int64_t* __restrict__ nid, int64_t batch, float grad_scale, float* __restrict__ loss,
-    int32_t* __restrict__ hit, float* __restrict__ gU, float* __restrict__ gI) {
+    int32_t* __restrict__ hit, float* __restrict__ gU, float* __restrict__ gI,
+    int32_t* __restrict__ err) {
   const int gl = threadIdx.x & 31;
   const int64_t group = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 5;
   const int64_t ngroups = (int64_t)gridDim.x * kBlock / 32;
+  int bad = 0;
   for (int64_t b = group; b < batch; b += ngroups) {
     const int64_t u = uid[b], p = pid[b], n = nid[b];
+    if (!in_rows(u, nu) || !in_rows(p, ni) || !in_rows(n, ni)) {  // uniform in the group
+      if (gl == 0) {
+        if (loss) loss[b] = __builtin_nanf("");
+        if (hit) hit[b] = 0;
+        bad += 1;
+      }
+      continue;
+    }
     const float* ur = U + u * d;
     const float* pr = I + p * d;
     const float* nr = I + n * d;
@@ -85,6 +98,7 @@ __global__ __launch_bounds__(kBlock) void bpr_kernel(
       }
     }
   }
+  if (bad && err) atomicAdd(err, bad);
 }
 
 // Dense Adam, elementwise, 4 floats per lane. Written as the same sequence of
@@ -171,12 +185,13 @@ extern "C" int dr_adam_rows(float* param, float* grad, float* exp_avg, float* ex
   return DR_OK;
 }
 
-extern "C" int dr_bpr_fwd_bwd(const float* user_table, const float* item_table, int64_t d,
+extern "C" int dr_bpr_fwd_bwd(const float* user_table, int64_t n_user_rows,
+                              const float* item_table, int64_t n_item_rows, int64_t d,
                               const int64_t* user_id, const int64_t* pos_id,
                               const int64_t* neg_id, int64_t batch, float grad_scale,
                               float* loss, int32_t* hit, float* grad_user, float* grad_item,
-                              dr_stream_t stream) {
-  DR_CHECK_ARG(batch >= 0, "batch must be >= 0");
+                              int32_t* err, dr_stream_t stream) {
+  DR_CHECK_ARG(batch >= 0 && n_user_rows >= 0 && n_item_rows >= 0, "sizes must be >= 0");
   if (batch == 0) return DR_OK;
   DR_CHECK_ARG(user_table && item_table && user_id && pos_id && neg_id, "null pointer");
   DR_CHECK_ARG(d >= 1 && d <= 512, "d must be in [1, 512]");
@@ -185,8 +200,8 @@ extern "C" int dr_bpr_fwd_bwd(const float* user_table, const float* item_table, 
   if (grid > 256 * 8) grid = 256 * 8;  // grid-stride the rest
 #define DR_BPR(EE)                                                                          \
   hipLaunchKernelGGL(bpr_kernel<EE>, dim3((unsigned)grid), dim3(kBlock), 0, s, user_table,  \
-                     item_table, d, user_id, pos_id, neg_id, batch, grad_scale, loss, hit,   \
-                     grad_user, grad_item)
+                     n_user_rows, item_table, n_item_rows, d, user_id, pos_id, neg_id, batch, \
+                     grad_scale, loss, hit, grad_user, grad_item, err)
   switch ((int)dr::ceil_div(d, 32)) {
     case 1: DR_BPR(1); break;
     case 2: DR_BPR(2); break;

@@ -28,14 +28,42 @@ __device__ __forceinline__ int64_t rec_at(const R* recs, int64_t i) {
   return (int64_t)recs[i];
 }
 
+// Id range check of one list (include/divrec_hip.h): true when every id is in
+// [0, n_items). Wave-wide (every lane gets the answer); the one-lane form
+// below serves the one-lane-per-user kernel.
+template <typename R>
+__device__ __forceinline__ bool wave_list_ok(const R* r, int k, int64_t n_items) {
+  bool bad = false;
+  for (int p = dr::lane_id(); p < k; p += 64) {
+    const int64_t v = rec_at(r, p);
+    bad |= v < 0 || v >= n_items;
+  }
+  return __ballot(bad) == 0ull;
+}
+template <typename R>
+__device__ __forceinline__ bool lane_list_ok(const R* r, int k, int64_t n_items) {
+  bool bad = false;
+  for (int p = 0; p < k; ++p) {
+    const int64_t v = rec_at(r, p);
+    bad |= v < 0 || v >= n_items;
+  }
+  return !bad;
+}
+
 // --------------------------------------------------------------- dense, float
 template <typename R, typename T, typename ACC>
 __global__ __launch_bounds__(256) void ild_dense_seq(const R* __restrict__ recs, int64_t n_users,
                                                      int k, const T* __restrict__ D,
-                                                     int64_t n_items, float* __restrict__ out) {
+                                                     int64_t n_items, float* __restrict__ out,
+                                                     int32_t* __restrict__ err) {
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (u >= n_users) return;
   const R* r = recs + u * k;
+  if (!lane_list_ok(r, k, n_items)) {
+    out[u] = __builtin_nanf("");
+    if (err) atomicAdd(err, 1);
+    return;
+  }
   ACC acc = 0;
   for (int p = 0; p < k; ++p) {
     const T* row = D + rec_at(r, p) * n_items;
@@ -48,11 +76,19 @@ __global__ __launch_bounds__(256) void ild_dense_seq(const R* __restrict__ recs,
 template <typename R, typename T>
 __global__ __launch_bounds__(256) void ild_dense_int(const R* __restrict__ recs, int64_t n_users,
                                                      int k, const T* __restrict__ D,
-                                                     int64_t n_items, float* __restrict__ out) {
+                                                     int64_t n_items, float* __restrict__ out,
+                                                     int32_t* __restrict__ err) {
   const int lane = dr::lane_id();
   const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   if (u >= n_users) return;
   const R* r = recs + u * k;
+  if (!wave_list_ok(r, k, n_items)) {  // wave-uniform
+    if (lane == 0) {
+      out[u] = __builtin_nanf("");
+      if (err) atomicAdd(err, 1);
+    }
+    return;
+  }
   long long acc = 0;
   for (int p = 0; p < k; ++p) {
     const T* row = D + rec_at(r, p) * n_items;
@@ -69,13 +105,21 @@ template <typename R>
 __global__ __launch_bounds__(256) void ild_labels_kernel(const R* __restrict__ recs,
                                                          int64_t n_users, int k,
                                                          const int64_t* __restrict__ labels,
-                                                         float* __restrict__ out) {
+                                                         int64_t n_items, float* __restrict__ out,
+                                                         int32_t* __restrict__ err) {
   __shared__ int64_t s_lab[4][kLabelMaxK];
   const int lane = dr::lane_id();
   const int wave = threadIdx.x >> 6;
   const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   if (u >= n_users) return;  // wave-uniform; no block barrier below
   const R* r = recs + u * k;
+  if (!wave_list_ok(r, k, n_items)) {  // wave-uniform
+    if (lane == 0) {
+      out[u] = __builtin_nanf("");
+      if (err) atomicAdd(err, 1);
+    }
+    return;
+  }
   int64_t* lab = s_lab[wave];
   for (int p = lane; p < k; p += 64) lab[p] = labels[rec_at(r, p)];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -136,7 +180,9 @@ template <typename R, int D>
 __global__ __launch_bounds__(256) void ild_embedding_kernel(const R* __restrict__ recs,
                                                             int64_t n_users, int k,
                                                             const __bf16* __restrict__ E,
-                                                            int kind, float* __restrict__ out) {
+                                                            int64_t n_items, int kind,
+                                                            float* __restrict__ out,
+                                                            int32_t* __restrict__ err) {
   __shared__ int64_t s_rows[4][kEmbMaxK];
   __shared__ float s_nsq[4][kEmbMaxK];
   const int lane = dr::lane_id();
@@ -145,6 +191,13 @@ __global__ __launch_bounds__(256) void ild_embedding_kernel(const R* __restrict_
   const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   if (u >= n_users) return;  // wave-uniform
   const R* r = recs + u * k;
+  if (!wave_list_ok(r, k, n_items)) {  // wave-uniform
+    if (lane == 0) {
+      out[u] = __builtin_nanf("");
+      if (err) atomicAdd(err, 1);
+    }
+    return;
+  }
   int64_t* rows = s_rows[wave];
   float* nsq = s_nsq[wave];
   for (int p = lane; p < k; p += 64) rows[p] = rec_at(r, p);
@@ -211,7 +264,9 @@ template <typename R, int D, int NT, int KIND>
 __global__ __launch_bounds__(256, 2) void ild_embedding_regs(const R* __restrict__ recs,
                                                           int64_t n_users, int k,
                                                           const __bf16* __restrict__ E,
-                                                          float* __restrict__ out) {
+                                                          int64_t n_items,
+                                                          float* __restrict__ out,
+                                                          int32_t* __restrict__ err) {
   constexpr int KS = D / 16;
   __shared__ float s_w[4][NT * 32];  // per row: 1/|e| (cosine) or |e|^2 (euclidean)
   const int lane = dr::lane_id();
@@ -220,6 +275,13 @@ __global__ __launch_bounds__(256, 2) void ild_embedding_regs(const R* __restrict
   const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   if (u >= n_users) return;  // wave-uniform
   const R* r = recs + u * k;
+  if (!wave_list_ok(r, k, n_items)) {  // wave-uniform
+    if (lane == 0) {
+      out[u] = __builtin_nanf("");
+      if (err) atomicAdd(err, 1);
+    }
+    return;
+  }
   float* w = s_w[wave];
   bf16x8 x[NT][KS];
 #pragma unroll
@@ -278,40 +340,37 @@ __global__ __launch_bounds__(256, 2) void ild_embedding_regs(const R* __restrict
 }
 
 template <typename R, int D, int KIND>
-void launch_regs_kind(const R* recs, int64_t n_users, int k, const __bf16* E, float* out,
-                      hipStream_t s, int grid) {
+void launch_regs_kind(const R* recs, int64_t n_users, int k, const __bf16* E, int64_t ni,
+                      float* out, int32_t* err, hipStream_t s, int grid) {
   switch ((k + 31) / 32) {
-    case 1: hipLaunchKernelGGL((ild_embedding_regs<R, D, 1, KIND>), grid, 256, 0, s, recs, n_users, k, E, out); break;
-    case 2: hipLaunchKernelGGL((ild_embedding_regs<R, D, 2, KIND>), grid, 256, 0, s, recs, n_users, k, E, out); break;
-    case 3: hipLaunchKernelGGL((ild_embedding_regs<R, D, 3, KIND>), grid, 256, 0, s, recs, n_users, k, E, out); break;
-    default: hipLaunchKernelGGL((ild_embedding_regs<R, D, 4, KIND>), grid, 256, 0, s, recs, n_users, k, E, out); break;
+    case 1: hipLaunchKernelGGL((ild_embedding_regs<R, D, 1, KIND>), grid, 256, 0, s, recs, n_users, k, E, ni, out, err); break;
+    case 2: hipLaunchKernelGGL((ild_embedding_regs<R, D, 2, KIND>), grid, 256, 0, s, recs, n_users, k, E, ni, out, err); break;
+    case 3: hipLaunchKernelGGL((ild_embedding_regs<R, D, 3, KIND>), grid, 256, 0, s, recs, n_users, k, E, ni, out, err); break;
+    default: hipLaunchKernelGGL((ild_embedding_regs<R, D, 4, KIND>), grid, 256, 0, s, recs, n_users, k, E, ni, out, err); break;
   }
 }
 
 template <typename R, int D>
-void launch_regs(const R* recs, int64_t n_users, int k, const __bf16* E, int kind, float* out,
-                 hipStream_t s, int grid) {
-  if (kind == DR_ILD_COSINE) launch_regs_kind<R, D, DR_ILD_COSINE>(recs, n_users, k, E, out, s, grid);
-  else if (kind == DR_ILD_DOT) launch_regs_kind<R, D, DR_ILD_DOT>(recs, n_users, k, E, out, s, grid);
-  else launch_regs_kind<R, D, DR_ILD_EUCLIDEAN>(recs, n_users, k, E, out, s, grid);
+void launch_regs(const R* recs, int64_t n_users, int k, const __bf16* E, int64_t ni, int kind,
+                 float* out, int32_t* err, hipStream_t s, int grid) {
+  if (kind == DR_ILD_COSINE) launch_regs_kind<R, D, DR_ILD_COSINE>(recs, n_users, k, E, ni, out, err, s, grid);
+  else if (kind == DR_ILD_DOT) launch_regs_kind<R, D, DR_ILD_DOT>(recs, n_users, k, E, ni, out, err, s, grid);
+  else launch_regs_kind<R, D, DR_ILD_EUCLIDEAN>(recs, n_users, k, E, ni, out, err, s, grid);
 }
 
 template <typename R>
-int launch_embedding(const R* recs, int64_t n_users, int k, const __bf16* E, int d, int kind,
-                     float* out, hipStream_t s) {
+int launch_embedding(const R* recs, int64_t n_users, int k, const __bf16* E, int64_t ni, int d,
+                     int kind, float* out, int32_t* err, hipStream_t s) {
   const int grid = (int)dr::ceil_div(n_users, 4);
   // the whole list fits in registers for d <= 128 (k <= 128 = 4 tiles)
   if (d == 32 || d == 64 || d == 128) {
-    if (d == 32) launch_regs<R, 32>(recs, n_users, k, E, kind, out, s, grid);
-    else if (d == 64) launch_regs<R, 64>(recs, n_users, k, E, kind, out, s, grid);
-    else launch_regs<R, 128>(recs, n_users, k, E, kind, out, s, grid);
+    if (d == 32) launch_regs<R, 32>(recs, n_users, k, E, ni, kind, out, err, s, grid);
+    else if (d == 64) launch_regs<R, 64>(recs, n_users, k, E, ni, kind, out, err, s, grid);
+    else launch_regs<R, 128>(recs, n_users, k, E, ni, kind, out, err, s, grid);
     return DR_OK;
   }
   switch (d) {
-    case 32: hipLaunchKernelGGL((ild_embedding_kernel<R, 32>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
-    case 64: hipLaunchKernelGGL((ild_embedding_kernel<R, 64>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
-    case 128: hipLaunchKernelGGL((ild_embedding_kernel<R, 128>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
-    case 256: hipLaunchKernelGGL((ild_embedding_kernel<R, 256>), grid, 256, 0, s, recs, n_users, k, E, kind, out); break;
+    case 256: hipLaunchKernelGGL((ild_embedding_kernel<R, 256>), grid, 256, 0, s, recs, n_users, k, E, ni, kind, out, err); break;
     default:
       dr::set_error("dr_ild_embedding: d must be one of 32, 64, 128, 256");
       return DR_EUNSUPPORTED;
@@ -321,30 +380,30 @@ int launch_embedding(const R* recs, int64_t n_users, int k, const __bf16* E, int
 
 template <typename R>
 int launch_dense(const R* recs, int64_t n_users, int k, const void* D, int dd, int64_t n_items,
-                 float* out, hipStream_t s) {
+                 float* out, int32_t* err, hipStream_t s) {
   switch (dd) {
     case DR_F32: {
       const int grid = (int)dr::ceil_div(n_users, 256);
       hipLaunchKernelGGL((ild_dense_seq<R, float, float>), grid, 256, 0, s, recs, n_users, k,
-                         (const float*)D, n_items, out);
+                         (const float*)D, n_items, out, err);
       break;
     }
     case DR_F64: {
       const int grid = (int)dr::ceil_div(n_users, 256);
       hipLaunchKernelGGL((ild_dense_seq<R, double, double>), grid, 256, 0, s, recs, n_users, k,
-                         (const double*)D, n_items, out);
+                         (const double*)D, n_items, out, err);
       break;
     }
     case DR_I32: {
       const int grid = (int)dr::ceil_div(n_users, 4);
       hipLaunchKernelGGL((ild_dense_int<R, int32_t>), grid, 256, 0, s, recs, n_users, k,
-                         (const int32_t*)D, n_items, out);
+                         (const int32_t*)D, n_items, out, err);
       break;
     }
     case DR_I64: {
       const int grid = (int)dr::ceil_div(n_users, 4);
       hipLaunchKernelGGL((ild_dense_int<R, int64_t>), grid, 256, 0, s, recs, n_users, k,
-                         (const int64_t*)D, n_items, out);
+                         (const int64_t*)D, n_items, out, err);
       break;
     }
     default:
@@ -358,56 +417,55 @@ int launch_dense(const R* recs, int64_t n_users, int k, const void* D, int dd, i
 
 extern "C" int dr_ild_dense(const void* recs, int rec_dtype, int64_t n_users, int k,
                             const void* dist, int dist_dtype, int64_t n_items, float* out,
-                            dr_stream_t stream) {
+                            int32_t* err, dr_stream_t stream) {
   DR_CHECK_ARG(k >= 1, "k must be >= 1");
   DR_CHECK_ARG(rec_dtype == DR_I32 || rec_dtype == DR_I64, "rec_dtype must be DR_I32/DR_I64");
   if (n_users == 0) return DR_OK;
   DR_CHECK_ARG(recs && dist && out, "null pointer");
   hipStream_t s = (hipStream_t)stream;
   int rc = rec_dtype == DR_I32
-               ? launch_dense((const int32_t*)recs, n_users, k, dist, dist_dtype, n_items, out, s)
-               : launch_dense((const int64_t*)recs, n_users, k, dist, dist_dtype, n_items, out, s);
+               ? launch_dense((const int32_t*)recs, n_users, k, dist, dist_dtype, n_items, out, err, s)
+               : launch_dense((const int64_t*)recs, n_users, k, dist, dist_dtype, n_items, out, err,
+                              s);
   if (rc != DR_OK) return rc;
   DR_CHECK_LAUNCH();
   return DR_OK;
 }
 
 extern "C" int dr_ild_labels(const void* recs, int rec_dtype, int64_t n_users, int k,
-                             const int64_t* labels, int64_t n_items, float* out,
+                             const int64_t* labels, int64_t n_items, float* out, int32_t* err,
                              dr_stream_t stream) {
   DR_CHECK_ARG(k >= 1 && k <= kLabelMaxK, "k must be in [1, 1024]");
   DR_CHECK_ARG(rec_dtype == DR_I32 || rec_dtype == DR_I64, "rec_dtype must be DR_I32/DR_I64");
-  (void)n_items;
   if (n_users == 0) return DR_OK;
   DR_CHECK_ARG(recs && labels && out, "null pointer");
   hipStream_t s = (hipStream_t)stream;
   const int grid = (int)dr::ceil_div(n_users, 4);
   if (rec_dtype == DR_I32)
     hipLaunchKernelGGL((ild_labels_kernel<int32_t>), grid, 256, 0, s, (const int32_t*)recs,
-                       n_users, k, labels, out);
+                       n_users, k, labels, n_items, out, err);
   else
     hipLaunchKernelGGL((ild_labels_kernel<int64_t>), grid, 256, 0, s, (const int64_t*)recs,
-                       n_users, k, labels, out);
+                       n_users, k, labels, n_items, out, err);
   DR_CHECK_LAUNCH();
   return DR_OK;
 }
 
 extern "C" int dr_ild_embedding(const void* recs, int rec_dtype, int64_t n_users, int k,
                                 const void* item_table, int64_t n_items, int d, int kind,
-                                float* out, dr_stream_t stream) {
+                                float* out, int32_t* err, dr_stream_t stream) {
   DR_CHECK_ARG(k >= 1 && k <= kEmbMaxK, "k must be in [1, 128]");
   DR_CHECK_ARG(rec_dtype == DR_I32 || rec_dtype == DR_I64, "rec_dtype must be DR_I32/DR_I64");
   DR_CHECK_ARG(kind == DR_ILD_COSINE || kind == DR_ILD_DOT || kind == DR_ILD_EUCLIDEAN,
                "unknown distance kind");
-  (void)n_items;
   if (n_users == 0) return DR_OK;
   DR_CHECK_ARG(recs && item_table && out, "null pointer");
   hipStream_t s = (hipStream_t)stream;
   int rc = rec_dtype == DR_I32
-               ? launch_embedding((const int32_t*)recs, n_users, k, (const __bf16*)item_table, d,
-                                  kind, out, s)
-               : launch_embedding((const int64_t*)recs, n_users, k, (const __bf16*)item_table, d,
-                                  kind, out, s);
+               ? launch_embedding((const int32_t*)recs, n_users, k, (const __bf16*)item_table,
+                                  n_items, d, kind, out, err, s)
+               : launch_embedding((const int64_t*)recs, n_users, k, (const __bf16*)item_table,
+                                  n_items, d, kind, out, err, s);
   if (rc != DR_OK) return rc;
   DR_CHECK_LAUNCH();
   return DR_OK;

@@ -37,18 +37,20 @@ _sz = ctypes.c_size_t
 SIGNATURES = {
     "dr_version": (_i32, []),
     "dr_last_error": (ctypes.c_char_p, []),
-    "dr_gather_dot": (_i32, [_p, _p, _i32, _i64, _p, _p, _i64, _p, _p]),
-    "dr_gather_dot_backward": (_i32, [_p, _p, _i64, _p, _p, _i64, _p, _p, _p, _p]),
+    "dr_gather_dot": (_i32, [_p, _i64, _p, _i64, _i32, _i64, _p, _p, _i64, _p, _p, _p]),
+    "dr_gather_dot_backward": (_i32, [_p, _i64, _p, _i64, _i64, _p, _p, _i64, _p, _p, _p, _p,
+                                      _p]),
     "dr_score_topk_workspace": (_sz, [_i64, _i64, _i32, _i32, _i32]),
     "dr_score_topk": (
         _i32,
         [_p, _p, _i64, _p, _i64, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _sz, _p],
     ),
     "dr_topk_merge": (_i32, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p]),
-    "dr_ild_dense": (_i32, [_p, _i32, _i64, _i32, _p, _i32, _i64, _p, _p]),
-    "dr_ild_labels": (_i32, [_p, _i32, _i64, _i32, _p, _i64, _p, _p]),
-    "dr_ild_embedding": (_i32, [_p, _i32, _i64, _i32, _p, _i64, _i32, _i32, _p, _p]),
-    "dr_bpr_fwd_bwd": (_i32, [_p, _p, _i64, _p, _p, _p, _i64, _f32, _p, _p, _p, _p, _p]),
+    "dr_ild_dense": (_i32, [_p, _i32, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
+    "dr_ild_labels": (_i32, [_p, _i32, _i64, _i32, _p, _i64, _p, _p, _p]),
+    "dr_ild_embedding": (_i32, [_p, _i32, _i64, _i32, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "dr_bpr_fwd_bwd": (_i32, [_p, _i64, _p, _i64, _i64, _p, _p, _p, _i64, _f32, _p, _p, _p, _p,
+                              _p, _p]),
     "dr_adam_dense": (_i32, [_p, _p, _p, _p, _i64, _f64, _f64, _f64, _f64, _f64, _i64, _p]),
     "dr_sample_pairwise": (_i32, [_p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_uint64, _p, _p,
                                   _p, _p, _p, _p, _p]),
@@ -133,6 +135,27 @@ def stream(device: torch.device) -> int:
 
 def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
+
+
+def error_counter(device: torch.device) -> torch.Tensor:
+    """A zeroed int32 device counter for the id range checks (include/divrec_hip.h)."""
+    return torch.zeros(1, dtype=torch.int32, device=device)
+
+
+def raise_if_out_of_range(err: Optional[torch.Tensor], what: str) -> None:
+    """Read an id-range error counter (one host sync) and raise IndexError, as
+    nn.Embedding / tensor indexing do in the reference, when it is non-zero."""
+    if err is not None:
+        n = int(err.item())
+        if n:
+            raise IndexError(f"index out of range in self ({what}: {n} entries with an id "
+                             f"outside the table)")
+
+
+def host_ids_in_range(ids: torch.Tensor, n_rows: int, what: str) -> None:
+    """Validate host (CPU) ids before they are uploaded: no device sync."""
+    if ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= n_rows):
+        raise IndexError(f"index out of range in self ({what})")
 
 
 def dtype_code(dt: torch.dtype) -> int:

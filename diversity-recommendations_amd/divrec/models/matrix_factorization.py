@@ -34,9 +34,10 @@ PRECISIONS = {"fp32": torch.float32, "bf16": torch.bfloat16}
 
 class _GatherDot(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, user_table, item_table, user_id, item_id):
+    def forward(ctx, user_table, item_table, user_id, item_id, checked):
         ctx.save_for_backward(user_table, item_table, user_id, item_id)
-        return ops.gather_dot(user_table, item_table, user_id, item_id)
+        # ids validated on the host need no device read-back of the counter
+        return ops.gather_dot(user_table, item_table, user_id, item_id, check=not checked)
 
     @staticmethod
     def backward(ctx, grad_out):
@@ -44,7 +45,7 @@ class _GatherDot(torch.autograd.Function):
         gu = torch.zeros_like(user_table) if ctx.needs_input_grad[0] else None
         gi = torch.zeros_like(item_table) if ctx.needs_input_grad[1] else None
         ops.gather_dot_backward(user_table, item_table, user_id, item_id, grad_out, gu, gi)
-        return gu, gi, None, None
+        return gu, gi, None, None, None
 
 
 def _on_device(model_device: torch.device, ids: torch.Tensor) -> torch.Tensor:
@@ -52,6 +53,17 @@ def _on_device(model_device: torch.device, ids: torch.Tensor) -> torch.Tensor:
     if ids.dtype != torch.int64:
         ids = ids.to(torch.int64)
     return ids.to(model_device, non_blocking=True)
+
+
+def _ids_for(model_device: torch.device, ids, n_rows: int, what: str):
+    """(device ids, validated on the host?): host ids are range-checked before
+    the upload (IndexError, as nn.Embedding raises), device ids in the kernel."""
+    ids = torch.as_tensor(ids)
+    host = ids.device.type == "cpu"
+    if host:
+        from divrec import _backend
+        _backend.host_ids_in_range(ids, n_rows, what)
+    return _on_device(model_device, ids), host
 
 
 class MatrixFactorization(RankingModel):
@@ -81,9 +93,10 @@ class MatrixFactorization(RankingModel):
         item_features: Optional[torch.Tensor] = None,
     ) -> torch.Tensor:
         dev = self._device()
-        uid = _on_device(dev, user_id)
-        iid = _on_device(dev, item_id)
-        return _GatherDot.apply(self.user_embeddings.weight, self.item_embeddings.weight, uid, iid)
+        uid, hu = _ids_for(dev, user_id, self.user_embeddings.num_embeddings, "user_id")
+        iid, hi = _ids_for(dev, item_id, self.item_embeddings.num_embeddings, "item_id")
+        return _GatherDot.apply(self.user_embeddings.weight, self.item_embeddings.weight, uid, iid,
+                                hu and hi)
 
     def scoring_tables(self, precision: str = "fp32") -> Tuple[torch.Tensor, torch.Tensor]:
         """The (user, item) tables score_topk scans at ``precision``: the

@@ -31,10 +31,16 @@ def gather_dot(
     item_table: torch.Tensor,
     user_id: torch.Tensor,
     item_id: torch.Tensor,
+    err: Optional[torch.Tensor] = None,
+    check: bool = True,
 ) -> torch.Tensor:
     """s[n] = <U[user_id[n]], I[item_id[n]]> (MatrixFactorization.forward,
     reference divrec/models/matrix_factorization.py:26-28). fp32 or bf16 tables,
-    int64 ids, fp32 output."""
+    int64 ids, fp32 output. Ids are range-checked on the device (an invalid
+    pair reads nothing and gives NaN): with ``check`` and no ``err`` this call
+    reads the count (one sync) and raises IndexError like nn.Embedding;
+    otherwise the count goes to the caller's ``err`` (may be None), which the
+    caller reads when it chooses (divrec._backend.raise_if_out_of_range)."""
     dev = B.require_device(user_table, item_table, user_id, item_id)
     _need(user_table.dim() == 2 and item_table.dim() == 2, "tables must be 2-D")
     _need(user_table.size(1) == item_table.size(1), "tables must share embedding_dim")
@@ -45,12 +51,17 @@ def gather_dot(
     _contig(user_table, "user_table"), _contig(item_table, "item_table")
     user_id, item_id = user_id.contiguous(), item_id.contiguous()
     out = torch.empty(user_id.numel(), dtype=torch.float32, device=dev)
+    own = err is None and check
+    if own:
+        err = B.error_counter(dev)
     rc = B.lib().dr_gather_dot(
-        user_table.data_ptr(), item_table.data_ptr(), B.dtype_code(user_table.dtype),
-        user_table.size(1), user_id.data_ptr(), item_id.data_ptr(), user_id.numel(),
-        out.data_ptr(), B.stream(dev),
+        user_table.data_ptr(), user_table.size(0), item_table.data_ptr(), item_table.size(0),
+        B.dtype_code(user_table.dtype), user_table.size(1), user_id.data_ptr(), item_id.data_ptr(),
+        user_id.numel(), out.data_ptr(), B.ptr(err), B.stream(dev),
     )
     B.check(rc, "dr_gather_dot")
+    if own:
+        B.raise_if_out_of_range(err, "dr_gather_dot")
     return out
 
 
@@ -62,8 +73,10 @@ def gather_dot_backward(
     grad_out: torch.Tensor,
     grad_user: Optional[torch.Tensor],
     grad_item: Optional[torch.Tensor],
+    err: Optional[torch.Tensor] = None,
 ) -> None:
-    """Accumulate dense fp32 embedding gradients of gather_dot in place."""
+    """Accumulate dense fp32 embedding gradients of gather_dot in place.
+    Out-of-range pairs add nothing and count in ``err`` (if given)."""
     dev = B.require_device(user_table, item_table, user_id, item_id, grad_out, grad_user, grad_item)
     _need(user_table.dtype == torch.float32 and item_table.dtype == torch.float32,
           "backward needs fp32 tables")
@@ -73,9 +86,10 @@ def gather_dot_backward(
                   f"{nm} must be a contiguous fp32 tensor shaped like its table")
     grad_out = grad_out.to(torch.float32).contiguous()
     rc = B.lib().dr_gather_dot_backward(
-        user_table.data_ptr(), item_table.data_ptr(), user_table.size(1),
-        user_id.contiguous().data_ptr(), item_id.contiguous().data_ptr(), user_id.numel(),
-        grad_out.data_ptr(), B.ptr(grad_user), B.ptr(grad_item), B.stream(dev),
+        user_table.data_ptr(), user_table.size(0), item_table.data_ptr(), item_table.size(0),
+        user_table.size(1), user_id.contiguous().data_ptr(), item_id.contiguous().data_ptr(),
+        user_id.numel(), grad_out.data_ptr(), B.ptr(grad_user), B.ptr(grad_item), B.ptr(err),
+        B.stream(dev),
     )
     B.check(rc, "dr_gather_dot_backward")
 
@@ -221,11 +235,13 @@ def ild_dense(recs: torch.Tensor, dist: torch.Tensor) -> torch.Tensor:
     out = torch.empty(n, dtype=torch.float32, device=dev)
     if n == 0:
         return out
+    err = B.error_counter(dev)
     rc = B.lib().dr_ild_dense(
         recs.data_ptr(), rc_dt, n, k, dist.data_ptr(), B.dtype_code(dist.dtype), dist.size(0),
-        out.data_ptr(), B.stream(dev),
+        out.data_ptr(), err.data_ptr(), B.stream(dev),
     )
     B.check(rc, "dr_ild_dense")
+    B.raise_if_out_of_range(err, "dr_ild_dense")
     return out
 
 
@@ -239,11 +255,13 @@ def ild_labels(recs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     out = torch.empty(n, dtype=torch.float32, device=dev)
     if n == 0:
         return out
+    err = B.error_counter(dev)
     rc = B.lib().dr_ild_labels(
         recs.data_ptr(), rc_dt, n, k, labels.data_ptr(), labels.numel(), out.data_ptr(),
-        B.stream(dev),
+        err.data_ptr(), B.stream(dev),
     )
     B.check(rc, "dr_ild_labels")
+    B.raise_if_out_of_range(err, "dr_ild_labels")
     return out
 
 
@@ -259,8 +277,11 @@ def _width_of(widths, d: int, what: str) -> int:
     raise ValueError(f"{what} supports embedding_dim <= {widths[-1]}, got {d}")
 
 
-def ild_embedding(recs: torch.Tensor, item_table: torch.Tensor, kind: str = "cosine") -> torch.Tensor:
-    """Per-user ILD with D computed from bf16 item embeddings (cosine/dot/euclidean)."""
+def ild_embedding(recs: torch.Tensor, item_table: torch.Tensor, kind: str = "cosine",
+                  check: bool = True) -> torch.Tensor:
+    """Per-user ILD with D computed from bf16 item embeddings (cosine/dot/euclidean).
+    A list with an id outside the table gives NaN; with ``check`` the call
+    reads the count (one sync) and raises IndexError."""
     dev = B.require_device(recs, item_table)
     recs, rc_dt = _recs(recs)
     _need(item_table.dtype == torch.bfloat16 and item_table.dim() == 2, "item_table must be bf16 2-D")
@@ -272,11 +293,13 @@ def ild_embedding(recs: torch.Tensor, item_table: torch.Tensor, kind: str = "cos
     out = torch.empty(n, dtype=torch.float32, device=dev)
     if n == 0:
         return out
+    err = B.error_counter(dev) if check else None
     rc = B.lib().dr_ild_embedding(
         recs.data_ptr(), rc_dt, n, k, item_table.data_ptr(), item_table.size(0),
-        item_table.size(1), _KINDS[kind], out.data_ptr(), B.stream(dev),
+        item_table.size(1), _KINDS[kind], out.data_ptr(), B.ptr(err), B.stream(dev),
     )
     B.check(rc, "dr_ild_embedding")
+    B.raise_if_out_of_range(err, "dr_ild_embedding")
     return out
 
 
@@ -290,9 +313,15 @@ def bpr_fwd_bwd(
     grad_scale: float,
     grad_user: Optional[torch.Tensor],
     grad_item: Optional[torch.Tensor],
+    err: Optional[torch.Tensor] = None,
+    check: bool = True,
 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Fused BPR forward + backward; returns per-triple (loss fp32, hit int32)
-    and accumulates dense gradients into grad_user / grad_item."""
+    and accumulates dense gradients into grad_user / grad_item. Ids are
+    range-checked on the device (an invalid triple adds nothing): with
+    ``check`` and no ``err`` the call reads the count (one sync) and raises
+    IndexError; otherwise the count goes to the caller's ``err`` (may be None),
+    checked by the caller (pair_wise_train_loop: once per epoch)."""
     dev = B.require_device(user_table, item_table, user_id, pos_id, neg_id, grad_user, grad_item)
     _need(user_table.dtype == torch.float32 and item_table.dtype == torch.float32, "fp32 tables")
     for t in (user_id, pos_id, neg_id):
@@ -301,13 +330,18 @@ def bpr_fwd_bwd(
     n = user_id.numel()
     loss = torch.empty(n, dtype=torch.float32, device=dev)
     hit = torch.empty(n, dtype=torch.int32, device=dev)
+    own = err is None and check
+    if own:
+        err = B.error_counter(dev)
     rc = B.lib().dr_bpr_fwd_bwd(
-        user_table.data_ptr(), item_table.data_ptr(), user_table.size(1),
-        user_id.contiguous().data_ptr(), pos_id.contiguous().data_ptr(),
+        user_table.data_ptr(), user_table.size(0), item_table.data_ptr(), item_table.size(0),
+        user_table.size(1), user_id.contiguous().data_ptr(), pos_id.contiguous().data_ptr(),
         neg_id.contiguous().data_ptr(), n, float(grad_scale), loss.data_ptr(), hit.data_ptr(),
-        B.ptr(grad_user), B.ptr(grad_item), B.stream(dev),
+        B.ptr(grad_user), B.ptr(grad_item), B.ptr(err), B.stream(dev),
     )
     B.check(rc, "dr_bpr_fwd_bwd")
+    if own:
+        B.raise_if_out_of_range(err, "dr_bpr_fwd_bwd")
     return loss, hit
 
 

@@ -23,7 +23,7 @@ import torch
 
 from torch.autograd.graph import increment_version
 
-from divrec import ops
+from divrec import _backend, ops
 from divrec.datasets import PairWiseDataset, PointWiseDataset, RankingDataset
 from divrec.losses import (
     LogSigmoidDifferenceLoss,
@@ -244,17 +244,25 @@ def pair_wise_train_loop(dataset: PairWiseDataset, model: RankingModel, loss: Pa
     fused = _bpr_fast_path(model, loss, scores)
     adam = _plain_adam(optimizer)
     lazy = fused and _plain_sparse_adam(optimizer)
+    epoch_err = None  # id range errors of the fused kernel, read once after the epoch
     for user_id, pos, neg, uf, pf, nf in dataset.loader(**loader_params):
         if fused:
             dev = model._device()
             U, I = model.user_embeddings.weight, model.item_embeddings.weight
+            if user_id.device.type == "cpu":  # host batches: raise before any compute
+                _backend.host_ids_in_range(user_id, U.size(0), "user_id")
+                _backend.host_ids_in_range(pos, I.size(0), "positive item_id")
+                _backend.host_ids_in_range(neg, I.size(0), "negative item_id")
             uid, pid, nid = (t.to(dev, torch.int64, non_blocking=True) for t in (user_id, pos, neg))
             if U.grad is None:
                 U.grad = torch.zeros_like(U)
             if I.grad is None:
                 I.grad = torch.zeros_like(I)
+            if epoch_err is None:
+                epoch_err = _backend.error_counter(dev)
             B = uid.numel()
-            losses_b, hits = ops.bpr_fwd_bwd(U.data, I.data, uid, pid, nid, 1.0 / B, U.grad, I.grad)
+            losses_b, hits = ops.bpr_fwd_bwd(U.data, I.data, uid, pid, nid, 1.0 / B, U.grad, I.grad,
+                                             err=epoch_err, check=False)
             loss_value = torch.sum(losses_b, dim=0) / B
             if lazy:  # touched rows only; the kernel zeroes those gradient rows
                 lazy_adam_step(optimizer, {U: torch.unique(uid),
@@ -280,6 +288,7 @@ def pair_wise_train_loop(dataset: PairWiseDataset, model: RankingModel, loss: Pa
             if n_scores:
                 batch_scores.append(torch.stack(
                     [s(positives.detach(), negatives.detach()).double() for s in scores]))
+    _backend.raise_if_out_of_range(epoch_err, "pair_wise_train_loop")
     count = len(batch_losses)
     # per-batch values summed as Python floats in batch order, like the reference
     mean_loss = sum(float(v) for v in torch.stack(batch_losses).double().cpu().tolist()) / count

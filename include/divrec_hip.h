@@ -48,14 +48,23 @@ int dr_version(void);
 const char* dr_last_error(void);
 
 /* ---------------------------------------------------------------------------
+ * Id range checks (all gather-type calls below): an id outside [0, rows) of
+ * its table — what nn.Embedding / tensor indexing reject with IndexError in
+ * the reference — is never dereferenced. The affected unit (pair, triple,
+ * user) produces NaN / adds nothing, and *err (caller-zeroed int32, may be
+ * NULL) is incremented once per such unit. The host raises IndexError when
+ * it reads a non-zero count.
+ *
  * MatrixFactorization.forward: s[n] = sum_d U[user_id[n], d] * I[item_id[n], d]
  * Replaces divrec/models/matrix_factorization.py:26-28 (two nn.Embedding
  * lookups + torch.sum(u * i, dim=1)). Tables row-major [rows, d], dtype
  * DR_F32 or DR_BF16 (both tables the same dtype); ids int64; out fp32 [n].
- * Ids are not range-checked on device (the host validates them).
+ * Runs of equal ids (RankingDataset's full((n,), u), PairWiseDataset's m x m
+ * pairs, divrec/datasets/base_datasets.py:94-107,165-171) read each row once.
  */
-int dr_gather_dot(const void* user_table, const void* item_table, int dtype, int64_t d,
-                  const int64_t* user_id, const int64_t* item_id, int64_t n, float* out,
+int dr_gather_dot(const void* user_table, int64_t n_user_rows, const void* item_table,
+                  int64_t n_item_rows, int dtype, int64_t d, const int64_t* user_id,
+                  const int64_t* item_id, int64_t n, float* out, int32_t* err,
                   dr_stream_t stream);
 
 /* Backward of dr_gather_dot into DENSE fp32 gradient tables (nn.Embedding with
@@ -64,10 +73,10 @@ int dr_gather_dot(const void* user_table, const void* item_table, int dtype, int
  *   grad_item[item_id[n]] += grad_out[n] * U[user_id[n]]
  * Accumulates with fp32 atomics (order-dependent in the last bits). Either
  * grad pointer may be NULL to skip that table. Tables must be DR_F32. */
-int dr_gather_dot_backward(const float* user_table, const float* item_table, int64_t d,
-                           const int64_t* user_id, const int64_t* item_id, int64_t n,
-                           const float* grad_out, float* grad_user, float* grad_item,
-                           dr_stream_t stream);
+int dr_gather_dot_backward(const float* user_table, int64_t n_user_rows, const float* item_table,
+                           int64_t n_item_rows, int64_t d, const int64_t* user_id,
+                           const int64_t* item_id, int64_t n, const float* grad_out,
+                           float* grad_user, float* grad_item, int32_t* err, dr_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Full-catalog scoring + top-K: for each of the n_users user rows, the k best
@@ -117,27 +126,29 @@ int dr_topk_merge(const float* in_scores, const int32_t* in_items, int parts, in
  * Intra-list diversity, IntraListDiversityScore.recommendations_loss with
  * reduction 'none' (divrec/losses/intra_list_diversity_score.py:20-42):
  *   out[u] = (sum_{p<q} D[r[u,p], r[u,q]]) / (k * (k - 1))     (k = 1 -> NaN)
- * `recs` [n_users, k] item ids of dtype rec_dtype (DR_I32 or DR_I64).
+ * `recs` [n_users, k] item ids of dtype rec_dtype (DR_I32 or DR_I64); a list
+ * holding an id outside [0, n_items) gives NaN and counts in *err (above).
  */
 
 /* Dense distance matrix D [n_items, n_items] (dtype DR_F32, DR_F64, DR_I32 or
  * DR_I64). Float D is accumulated in its own precision in itertools.combinations order, like the
  * reference's Python sum (bit-exact); integer D is summed exactly. */
 int dr_ild_dense(const void* recs, int rec_dtype, int64_t n_users, int k, const void* dist,
-                 int dist_dtype, int64_t n_items, float* out, dr_stream_t stream);
+                 int dist_dtype, int64_t n_items, float* out, int32_t* err, dr_stream_t stream);
 
 /* Label equality D[i,j] = (label[i] == label[j]), the matrix of
  * IntraListBinaryUnfairnessScore.get_distance_matrix (:60-63), computed on the
  * fly from labels int64 [n_items] (exact integer count). */
 int dr_ild_labels(const void* recs, int rec_dtype, int64_t n_users, int k,
-                  const int64_t* labels, int64_t n_items, float* out, dr_stream_t stream);
+                  const int64_t* labels, int64_t n_items, float* out, int32_t* err,
+                  dr_stream_t stream);
 
 /* Distance computed on the fly from an item embedding table (bf16 [n_items, d],
  * d in {32, 64, 128, 256}, k <= 128) by a bf16 MFMA Gram tile per user
  * (kind: enum dr_ild_kind). fp32 accumulation. */
 int dr_ild_embedding(const void* recs, int rec_dtype, int64_t n_users, int k,
                      const void* item_table, int64_t n_items, int d, int kind, float* out,
-                     dr_stream_t stream);
+                     int32_t* err, dr_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * BPR step (pair_wise_train_loop, divrec/train/utils.py:144-152, with
@@ -147,11 +158,14 @@ int dr_ild_embedding(const void* recs, int rec_dtype, int64_t n_users, int k,
  *   g = -sigmoid(-x) * grad_scale  (grad_scale = 1/B for the 'mean' reduction)
  *   grad_user[u] += g (I[p] - I[n]); grad_item[p] += g U[u]; grad_item[n] -= g U[u]
  * fp32 tables [*, d]; ids int64 [B]; loss fp32 [B] and hit int32 [B] may be
- * NULL. Gradients are DENSE fp32 tables accumulated with atomics. */
-int dr_bpr_fwd_bwd(const float* user_table, const float* item_table, int64_t d,
-                   const int64_t* user_id, const int64_t* pos_id, const int64_t* neg_id,
-                   int64_t batch, float grad_scale, float* loss, int32_t* hit,
-                   float* grad_user, float* grad_item, dr_stream_t stream);
+ * NULL. Gradients are DENSE fp32 tables accumulated with atomics. A triple
+ * with an out-of-range id adds nothing, gets loss NaN / hit 0 and counts in
+ * *err (id range checks, above). */
+int dr_bpr_fwd_bwd(const float* user_table, int64_t n_user_rows, const float* item_table,
+                   int64_t n_item_rows, int64_t d, const int64_t* user_id,
+                   const int64_t* pos_id, const int64_t* neg_id, int64_t batch,
+                   float grad_scale, float* loss, int32_t* hit, float* grad_user,
+                   float* grad_item, int32_t* err, dr_stream_t stream);
 
 /* Dense Adam step in fp32 over n elements, the update torch.optim.Adam
  * (amsgrad=False, maximize=False) applies at divrec/train/utils.py:151:

@@ -203,6 +203,22 @@ def test_scoring_tables_follow_fused_training():
         assert torch.equal(got, want), precision
 
 
+def test_pair_wise_train_loop_out_of_range_raises():
+    """A batch with an item id outside the model's table: the reference's
+    nn.Embedding raises IndexError; so does the fused loop (host batches are
+    checked before the upload)."""
+    data = datasets.UserItemInteractionsDataset(
+        torch.LongTensor([[0, 1], [1, 2], [1, 30]]), number_of_users=2, number_of_items=31,
+        user_features=datasets.Features(torch.zeros(2, 1), ["x"]),
+        item_features=datasets.Features(torch.zeros(31, 1), ["x"]))
+    mf = models.MatrixFactorization(2, 20, 16).to(DEV)  # fewer items than the data
+    opt = torch.optim.Adam(mf.parameters(), lr=1e-2)
+    random.seed(1)
+    with pytest.raises(IndexError):
+        train.pair_wise_train_loop(datasets.PairWiseDataset(data, max_sampled=3), mf,
+                                   losses.LogSigmoidDifferenceLoss(), opt, batch_size=4)
+
+
 def test_recommendations_ragged_lists_raise_like_reference():
     """A user with fewer candidates than k: the reference's
     torch.LongTensor(recommendations) raises on ragged lists (utils.py:77);

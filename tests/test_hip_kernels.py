@@ -58,6 +58,96 @@ def test_gather_dot_integer_exact():
     assert np.array_equal(got.cpu().numpy(), oracle.mf_forward(U, I, uid, iid))
 
 
+def _run_ids(rng, n, n_rows, max_run):
+    """Ids in runs of random length 1..max_run (runs straddle every unroll
+    and span boundary of the gather)."""
+    out = []
+    while len(out) < n:
+        out += [int(rng.integers(0, n_rows))] * int(rng.integers(1, max_run + 1))
+    return np.asarray(out[:n], dtype=np.int64)
+
+
+@pytest.mark.parametrize("pattern", ["full", "mxm", "runs"])
+@pytest.mark.parametrize("d,dtype", [(100, "f32"), (128, "f32"), (64, "bf16"), (100, "bf16"),
+                                     (256, "bf16")])
+def test_gather_dot_run_patterns(pattern, d, dtype):
+    """The reference's own call patterns, whose repeated rows the gather reads
+    once per run: RankingDataset's (torch.full((n,), u), candidates)
+    (base_datasets.py:165-171), PairWiseDataset's m x m product, model(u, pos)
+    and model(u, neg) (:94-107), and random run lengths. Same tolerance as
+    test_gather_dot."""
+    rng = np.random.default_rng(d + len(pattern))
+    nu, ni = 300, 4000
+    U = rng.standard_normal((nu, d)).astype(np.float32)
+    I = rng.standard_normal((ni, d)).astype(np.float32)
+    if dtype == "bf16":
+        U, I = oracle.as_bf16_f32(U), oracle.as_bf16_f32(I)
+    if pattern == "full":
+        uid = np.full(ni - 37, 7, dtype=np.int64)
+        iid = np.setdiff1d(np.arange(ni), rng.choice(ni, 37, replace=False)).astype(np.int64)
+    elif pattern == "mxm":
+        m, users = 20, rng.choice(nu, 97, replace=False)
+        pos = rng.integers(0, ni, (97, m))
+        neg = rng.integers(0, ni, (97, m))
+        uid = np.repeat(users, m * m)
+        iid = np.concatenate([np.repeat(pos, m, axis=1).ravel(),  # model(u, pos): p_a m times
+                              np.tile(neg, (1, m)).ravel()])      # model(u, neg): cycling
+        uid = np.concatenate([uid, uid])
+    else:
+        n = 50_003
+        uid, iid = _run_ids(rng, n, nu, 9), _run_ids(rng, n, ni, 5)
+    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+    got = ops.gather_dot(torch.from_numpy(U).to(DEV).to(tdt), torch.from_numpy(I).to(DEV).to(tdt),
+                         torch.from_numpy(uid).to(DEV), torch.from_numpy(iid).to(DEV)).cpu().numpy()
+    ref = oracle.mf_forward(U, I, uid, iid)
+    scale = np.abs(U[uid] * I[iid]).max(axis=1) * d
+    assert np.all(np.abs(got - ref) <= 4e-7 * scale + 1e-6)
+
+
+def test_ids_out_of_range_raise_index_error():
+    """nn.Embedding / tensor indexing raise IndexError on an id outside the
+    table (the reference's behaviour); the kernels never read such a row:
+    gather_dot, the MF forward on host and device ids, the fused BPR step,
+    the training loop and the three ILD modes."""
+    from divrec import _backend, models
+    rng = np.random.default_rng(0)
+    U = torch.from_numpy(rng.standard_normal((10, 32)).astype(np.float32)).to(DEV)
+    I = torch.from_numpy(rng.standard_normal((20, 32)).astype(np.float32)).to(DEV)
+    ok = torch.arange(5, device=DEV)
+    for bad_u, bad_i in (([0, 10, 2, 3, 4], ok), (ok, [0, 1, -1, 3, 4]), (ok, [0, 1, 2, 3, 20])):
+        bu = torch.as_tensor(bad_u, device=DEV)
+        bi = torch.as_tensor(bad_i, device=DEV)
+        with pytest.raises(IndexError):
+            ops.gather_dot(U, I, bu, bi)
+        with pytest.raises(IndexError):
+            ops.bpr_fwd_bwd(U, I, bu, bi, ok, 0.2, torch.zeros_like(U), torch.zeros_like(I))
+    err = _backend.error_counter(torch.device(DEV))
+    out = ops.gather_dot(U, I, torch.tensor([0, 10, 2], device=DEV),
+                         torch.tensor([0, 1, 2], device=DEV), err=err, check=False)
+    assert int(err.item()) == 1 and torch.isnan(out[1]) and not torch.isnan(out[[0, 2]]).any()
+    gU, gI = torch.zeros_like(U), torch.zeros_like(I)
+    ops.bpr_fwd_bwd(U, I, torch.tensor([0, 99], device=DEV), torch.tensor([1, 1], device=DEV),
+                    torch.tensor([2, 2], device=DEV), 1.0, gU, gI, err=err, check=False)
+    assert int(err.item()) == 2 and not gU[1:].any()  # the bad triple added nothing
+    mf = models.MatrixFactorization(10, 20, 32).to(DEV)
+    for uid, iid in (([0, 10], [0, 1]), ([0, 1], [0, 25])):
+        with pytest.raises(IndexError):  # host ids: checked before the upload
+            mf(torch.LongTensor(uid), torch.LongTensor(iid))
+        with pytest.raises(IndexError):  # device ids: checked by the kernel
+            mf(torch.tensor(uid, device=DEV), torch.tensor(iid, device=DEV))
+    recs = torch.tensor([[0, 1, 2], [3, -1, 4]], device=DEV)
+    with pytest.raises(IndexError):
+        ops.ild_dense(recs, torch.rand(20, 20, device=DEV))
+    with pytest.raises(IndexError):
+        ops.ild_dense(recs, torch.randint(0, 5, (20, 20), device=DEV))
+    with pytest.raises(IndexError):
+        ops.ild_labels(recs, torch.randint(0, 3, (20,), device=DEV))
+    with pytest.raises(IndexError):
+        ops.ild_embedding(recs, I.to(torch.bfloat16))
+    vals = ops.ild_embedding(recs, I.to(torch.bfloat16), check=False)
+    assert not torch.isnan(vals[0]) and torch.isnan(vals[1])
+
+
 @pytest.mark.parametrize("d", [32, 64, 100, 128, 300])
 def test_gather_dot_backward(d):
     rng = np.random.default_rng(3 + d)

@@ -55,7 +55,7 @@ def test_argument_errors_without_gpu():
     rc = lib.dr_score_topk(None, None, 10, None, 10, 0, _backend.DR_I32, 64, 10, None, None, None,
                            None, None, 0, None)
     assert rc == -1 and b"DR_BF16 or DR_F32" in lib.dr_last_error()
-    rc = lib.dr_ild_embedding(None, 3, 5, 500, None, 10, 128, 0, None, None)
+    rc = lib.dr_ild_embedding(None, 3, 5, 500, None, 10, 128, 0, None, None, None)
     assert rc == -1
     rc = lib.dr_topk_merge(None, None, 3, 10, 1000, 2000, None, None, None)
     assert rc == -1 and b"k_out must be <= 1024" in lib.dr_last_error()
@@ -64,7 +64,9 @@ def test_argument_errors_without_gpu():
     rc = lib.dr_mmr_rerank(None, None, 4, 2000, None, 10, 128, 10, 0.5, None, None)
     assert rc == -1 and b"C must be" in lib.dr_last_error()
     # empty inputs are a no-op success
-    assert lib.dr_gather_dot(None, None, 0, 64, None, None, 0, None, None) == 0
+    assert lib.dr_gather_dot(None, 0, None, 0, 0, 64, None, None, 0, None, None, None) == 0
+    rc = lib.dr_gather_dot(None, -1, None, 0, 0, 64, None, None, 3, None, None, None)
+    assert rc == -1 and b"sizes" in lib.dr_last_error()
 
 
 def test_workspace_query_is_host_only():
