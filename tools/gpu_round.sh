@@ -13,3 +13,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT
 cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python bench.py --workload score1m > gpurun_out/wl_score1m.json 2> gpurun_out/wl_score1m.err
 timeout -k 10 300 python bench.py --workload mmr > gpurun_out/wl_mmr.json 2> gpurun_out/wl_mmr.err
+timeout -k 10 300 python bench.py --workload gather > gpurun_out/wl_gather.json 2> gpurun_out/wl_gather.err
+timeout -k 10 300 python bench.py --workload bpr > gpurun_out/wl_bpr.json 2> gpurun_out/wl_bpr.err
