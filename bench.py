@@ -264,6 +264,35 @@ def load_traffic(cfg_key: str):
     return None
 
 
+def pmc_traffic(workload: str, config: str, kernel: str, group: int = 0, per_step: int = 1):
+    """HBM bytes per step of one kernel from a committed per-dispatch PMC
+    summary (tools/gpu_pmc_kernels.sh -> tools/pmc_kernels.py ->
+    profiles/pmc_<workload>.json), read only when its config matches. The
+    kernel's dispatches come in groups of `reps` calls (one group per phase
+    of the workload, in launch order); `per_step` = dispatches per call."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if rec.get("config") != config:
+        return None
+    reps, total, found = int(rec["reps"]), 0.0, False
+    for prefix in kernel.split("|"):  # every instantiation of every named kernel
+        for name, k in rec["kernels"].items():
+            if not name.startswith(prefix):
+                continue
+            part = k["hbm_bytes"][group * reps * per_step:(group + 1) * reps * per_step]
+            if len(part) != reps * per_step:
+                return None
+            total, found = total + sum(part) / reps, True
+    return total if found else None
+
+
+SCAN_KERNELS = "score_scan_kernel|sample_rows_kernel|topk_threshold_kernel|topk_finalize_kernel"
+
+
 def time_layout(args, world: int, dev, S: int, record_recs: bool = True):
     """Time the catalog step on a (world/S) x S grid of ranks: warmup, barrier,
     exactly args.steps timed steps, barrier; max over ranks. Returns a dict
@@ -351,7 +380,7 @@ def main():
     cfg_key = f"U{U_n}_I{I_n}_d{d}_k{k}_G{world}"
     flops = 2.0 * (u_hi - u_lo) * (hi - lo) * d
     achieved = flops / r["topk_s"] / 1e12
-    traffic = load_traffic(cfg_key)
+    traffic = pmc_traffic("catalog", cfg_key, SCAN_KERNELS) or load_traffic(cfg_key)
     result = {
         "metric": "scored pairs/sec + ILD-eval users/sec, 1M x 10M d=128 at 1/2/4/8 GPU",
         "value": U_n * I_n / step_s,
@@ -375,6 +404,10 @@ def main():
             "item_shards": S,
         },
         "ild_users_per_s": U_n / r["ild_max"],
+        "ild_roofline": dict(_hbm(U_n // world * (k * 8 + k * d * 2 + 4), r["ild_max"],
+                                  pmc_traffic("catalog", cfg_key, "ild_embedding_regs")),
+                             kernel="dr_ild_embedding (cosine)",
+                             per_unit=f"{k * 8 + k * d * 2 + 4} B/user = k ids + k bf16 rows + out"),
         "score_topk_ms": r["topk_s"] * 1e3,
         "score_topk_ms_max_over_ranks": r["topk_max"] * 1e3,
         "ild_ms": r["ild_max"] * 1e3,
@@ -570,7 +603,9 @@ def secondary(args):
             pw, pdt = _timed(lambda: ops.gather_dot(Ut, It, pu, pi, check=False), args.steps,
                              args.warmup)
             nb = run_bytes(pu, pi)
-            patterns[name] = dict(_hbm(nb, pdt), pairs=pu.numel(), pairs_per_s=pu.numel() / pw,
+            patterns[name] = dict(_hbm(nb, pdt, pmc_traffic("gather", "gather", "gather_dot_runs",
+                                                            group=1 + len(patterns))),
+                                  pairs=pu.numel(), pairs_per_s=pu.numel() / pw,
                                   ms=pdt * 1e3, bytes_per_pair=nb / pu.numel(),
                                   per_unit="2 ids x 8 B + 4 B out per pair + d x 4 B per "
                                            "user run for its user row and each distinct item")
@@ -585,7 +620,8 @@ def secondary(args):
         added = 2 * d * 4 * n
         backward = {"value": n / bwall, "unit": "pairs/s", "ms": bdt * 1e3,
                     "kernel": "dr_gather_dot_backward",
-                    "hbm_roofline": _hbm((2 * d * 4 + 2 * 8 + 4) * n + added, bdt),
+                    "hbm_roofline": _hbm((2 * d * 4 + 2 * 8 + 4) * n + added, bdt,
+                                         pmc_traffic("gather", "gather", "gather_dot_bwd_rows")),
                     "atomic_roofline": {"bound": "fp32 atomics", "added_bytes": added,
                                         "achieved": added / bdt / 1e9, "peak": ATOMIC_F32_GBS,
                                         "unit": "GB/s", "frac": added / bdt / 1e9 / ATOMIC_F32_GBS}}
@@ -593,7 +629,8 @@ def secondary(args):
               "pairs/s", args, wall, "f32",
               {"workload": f"dr_gather_dot, {n} uniform random (user, item) pairs, fp32 tables "
                            f"{U_n}x{d} and {I_n}x{d}", "pairs": n, "dim": d},
-              dict(_hbm(per_pair * n, dt), kernel="dr_gather_dot",
+              dict(_hbm(per_pair * n, dt, pmc_traffic("gather", "gather", "gather_dot_runs")),
+                   kernel="dr_gather_dot",
                    per_unit=f"{per_pair} B/pair = 2 rows x {d} x 4 B + 2 ids x 8 B + 4 B out"),
               cpu, backward=backward, patterns=patterns)
         return 0
@@ -675,7 +712,9 @@ def secondary(args):
         lazy = {"value": B / lwall, "unit": "triples/s", "ms_per_step": lwall * 1e3,
                 "unique_ms": tu * 1e3, "adam_rows_ms": tr * 1e3,
                 "touched_rows": {"users": nrows[0], "items": nrows[1]},
-                "adam_rows_roofline": dict(_hbm(rows_bytes, tr), kernel="dr_adam_rows",
+                "adam_rows_roofline": dict(_hbm(rows_bytes, tr, pmc_traffic("bpr", "bpr", "adam_rows_kernel",
+                                                                            per_step=2)),
+                                           kernel="dr_adam_rows",
                                            per_unit=f"{8 * d * 4 + 8} B/touched row"),
                 "note": "torch.optim.SparseAdam semantics over the touched rows; the reference "
                         "trains with dense Adam, which the headline BPR value above reproduces"}
@@ -707,10 +746,11 @@ def secondary(args):
                            f"positive from a {npos}-item/user CSR, uniform negative) + "
                            f"dr_adam_dense over both fp32 tables", "users": U_n, "items": I_n,
                "dim": d, "batch": B},
-              dict(_hbm(per_triple * B, tb), kernel="dr_bpr_fwd_bwd",
+              dict(_hbm(per_triple * B, tb, pmc_traffic("bpr", "bpr", "bpr_kernel")),
+                   kernel="dr_bpr_fwd_bwd",
                    per_unit=f"{per_triple} B/triple"),
               cpu, bpr_ms=tb * 1e3, adam_ms=ta * 1e3, lazy_adam_step=lazy, sampler=sampler,
-              adam_roofline=_hbm(adam_bytes, ta),
+              adam_roofline=_hbm(adam_bytes, ta, pmc_traffic("bpr", "bpr", "adam_kernel", per_step=2)),
               # the fused kernel's real ceiling: fp32 atomics execute at the memory
               # side at ~1.3 TB/s of added bytes chip-wide (MI355X_MICROARCH.md,
               # Global float atomics); it adds 3 rows of d fp32 per triple
@@ -815,9 +855,14 @@ def mmr_pipeline(args):
            "mmr_users_per_s": n_r / mmr_s, "mean_ild": float(out["mean"]),
            "roofline": {"bound": "mfma", "achieved": flops / topk_s / 1e12,
                         "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": flops / topk_s / 1e12 / MFMA_BF16_PEAK_TFLOPS, "traffic": None,
+                        "frac": flops / topk_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+                        "traffic": pmc_traffic("mmr", f"mmr_U{U_n}_I{I_n}_d{d}_C{C}_k{kout}",
+                                               SCAN_KERNELS) if world == 1 else None,
                         "kernel": f"dr_score_topk k={C} (the step's dominant kernel)"},
-           "mmr_roofline": dict(_hbm(per_user * n_r, mmr_s), kernel="dr_mmr_rerank",
+           "mmr_roofline": dict(_hbm(per_user * n_r, mmr_s,
+                                     pmc_traffic("mmr", f"mmr_U{U_n}_I{I_n}_d{d}_C{C}_k{kout}",
+                                                 "mmr_probe_kernel") if world == 1 else None),
+                                kernel="dr_mmr_rerank",
                                 per_unit=f"{per_user} B/user"),
            "cpu_baseline": cpu}
     if rank == 0:
