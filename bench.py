@@ -55,6 +55,7 @@ from divrec.distributed import (exchange_partials, global_mean, grid_layout,  # 
                                 shard_range)
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32 (= the fp32 vector rate, MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 ATOMIC_F32_GBS = 1300.0  # chip-wide global_atomic_add_f32 rate (MI355X_MICROARCH.md)
 
@@ -84,7 +85,7 @@ def parse():
                     help="after timing, recompute this many of each rank's final users "
                          "over the whole catalog on one device and require identical lists")
     ap.add_argument("--workload", default="catalog",
-                    choices=["catalog", "score1m", "gather", "bpr", "mmr"])
+                    choices=["catalog", "score1m", "gather", "bpr", "mmr", "fp32"])
     ap.add_argument("--candidates", type=int, default=1000, help="mmr: top-C candidates per user")
     ap.add_argument("--mmr-k", type=int, default=100, help="mmr: re-ranked list length")
     ap.add_argument("--mmr-lambda", type=float, default=0.5)
@@ -495,7 +496,12 @@ def _timed(fn, steps: int, warmup: int):
 
 def _line(metric, value, unit, args, step_s, dtype, config, roofline, cpu, **extra):
     dev = torch.device("cuda", 0)
-    with_measured(roofline, dev, "mfma_bf16_tflops" if roofline["bound"] == "mfma" else "hbm_copy_gbs")
+    if roofline.get("peak") == MFMA_F32_PEAK_TFLOPS:  # fp32 MFMA: the guide's measured rate
+        roofline.update(peak_achievable=155.0, frac_of_achievable=roofline["achieved"] / 155.0,
+                        achievable_source="MI355X_MICROARCH.md (v_mfma_f32_32x32x2_f32, 155 TF)")
+    else:
+        with_measured(roofline, dev,
+                      "mfma_bf16_tflops" if roofline["bound"] == "mfma" else "hbm_copy_gbs")
     for v in extra.values():
         if isinstance(v, dict) and v.get("bound") == "hbm":
             with_measured(v, dev, "hbm_copy_gbs")
@@ -550,6 +556,30 @@ def secondary(args):
                "unit": "TFLOP/s", "frac": flops / dt / 1e12 / MFMA_BF16_PEAK_TFLOPS,
                "traffic": load_traffic(f"U{U_n}_I{I_n}_d{d}_k{k}_G1"),
                "kernel": "dr_score_topk (sample scan + thresholds + seeded scan + finalize)"}, cpu)
+        return 0
+
+    if args.workload == "fp32":
+        # MatrixFactorization.score_topk's default (fp32-faithful) mode on the
+        # reference experiments' own width, d = 100 (zero-padded to 128 once
+        # per parameter version, as the model does): exact fp32 products and
+        # fp32 sums on v_mfma_f32_32x32x2_f32
+        U_n, I_n, d, k = 262_144, 1_000_000, 100, 100
+        w = ops.score_width(torch.float32, d)
+        users = ops.pad_columns(torch.randn(U_n, d, generator=g, device=dev), w)
+        items = ops.pad_columns(torch.randn(I_n, d, generator=g, device=dev), w)
+        wall, dt = _timed(lambda: ops.score_topk(users, items, k), args.steps, args.warmup)
+        flops_pad = 2.0 * U_n * I_n * w
+        _line("fp32-faithful scored pairs/sec, d=100 (MatrixFactorization default scoring mode)",
+              U_n * I_n / wall, "scored pairs/s", args, wall, "f32",
+              {"workload": f"score_topk on fp32 tables {U_n} users x {I_n} items, d={d} "
+                           f"zero-padded to {w}, k={k}", "users": U_n, "items": I_n, "dim": d,
+               "scan_width": w, "k": k},
+              {"bound": "mfma", "achieved": flops_pad / dt / 1e12, "peak": MFMA_F32_PEAK_TFLOPS,
+               "unit": "TFLOP/s", "frac": flops_pad / dt / 1e12 / MFMA_F32_PEAK_TFLOPS,
+               "traffic": None, "flop_per_launch": flops_pad,
+               "kernel": "dr_score_topk, fp32 scan (v_mfma_f32_32x32x2_f32) + finalize; flops "
+                         "counted at the padded width"},
+              None, useful_tflops=2.0 * U_n * I_n * d / dt / 1e12)
         return 0
 
     if args.workload == "gather":

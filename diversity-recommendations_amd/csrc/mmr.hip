@@ -19,8 +19,9 @@
 //     BOUND: the picks are exactly the eager greedy's. No barrier per round.
 //   * When a probe no longer beats BOUND (or after round 0, whose max term is
 //     0), the batch ends: every candidate folds the batch's picked columns into
-//     its max term and a new batch starts. ~9 batches for 100 picks of 1000
-//     random candidates (lambda = 0.5).
+//     its max term and a new batch starts. ~9.6 batches for 100 picks of 1000
+//     random candidates (lambda = 0.5), ~12.6 on real top-1000 lists.
+// The kernel below is the round-2 layout of this design (mmr_batch_kernel).
 #include "common.h"
 
 namespace {
@@ -74,50 +75,124 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return dr::readlane_u64(v, 63);
 }
 
+
+// a[lane] max a[lane ^ 32] (v_permlane32_swap: one VALU, no LDS round trip)
+__device__ __forceinline__ float half_swap_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// Diagnostic build (-DDR_MMR_DIAG, a measurement variant library only):
+// per-wave s_memtime cycles of each phase, summed over users into a device
+// array that dr_mmr_diag_read copies out. Never in the product library.
+#ifdef DR_MMR_DIAG
+__device__ unsigned long long g_mmr_diag[kWaves][16];
+#define MG_T0(v) uint64_t v = __builtin_amdgcn_s_memtime()
+#define MG_ADD(slot, t0) dg[slot] += __builtin_amdgcn_s_memtime() - (t0)
+#else
+#define MG_T0(v) ((void)0)
+#define MG_ADD(slot, t0) ((void)0)
+#endif
+enum { kMgLoad, kMgSelect, kMgStage, kMgMma, kMgSync1, kMgRounds, kMgSync2, kMgFold, kMgBatches,
+       kMgTotal, kMgStageBar, kMgGt, kMgSlots = 16 };
+
+// Max over the wave's 64 lanes (lanes = 64) or over lanes 0..31 (lanes = 32)
+// by fused v_max_u32_dpp steps (one VALU each: the reduction is the latency
+// of the serial chains below); the result is read from the last lane.
+template <int LANES>
+__device__ __forceinline__ uint32_t wmax_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, true));
+  if constexpr (LANES == 64) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, true));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  } else {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+  }
+}
+
+// Round-2 layout of the probe-batch kernel: the same probes, bound and exact
+// fast rounds as mmr_probe_kernel (identical picks), rebuilt around latency:
+//   * the batch's 32 similarity columns stay where the MFMAs leave them
+//     (4 accumulators = 64 VGPRs per lane) instead of 128 KB of LDS; the fold
+//     reads the picked columns there (constant register pattern per lane
+//     half, one v_permlane32_swap per tile);
+//   * probe selection ranks by the 32-bit value order (fused-DPP max, one
+//     VALU per step), falling back to the exact 64-bit (value, position) key
+//     only when two lanes tie on the value; the winner's owners stage its row
+//     at once (the winner's tile and lane are uniform), so no probe-slot map
+//     is read back from LDS;
+//   * per-candidate score, 1/|e| and id live in LDS (registers hold the rows
+//     and the columns).
+// Out-of-range ids (>= n_items) are counted in *err and never picked.
 template <int D>
-__global__ __launch_bounds__(kThreads) void mmr_probe_kernel(
+__global__ __launch_bounds__(kThreads) void mmr_batch_kernel(
     const int32_t* __restrict__ cand_items, const float* __restrict__ cand_scores, int C,
-    const __bf16* __restrict__ E, int k_out, float lambda, int32_t* __restrict__ out_items) {
+    const __bf16* __restrict__ E, int64_t n_items, int k_out, float lambda,
+    int32_t* __restrict__ out_items, int32_t* __restrict__ err) {
   constexpr int KS = D / 16;  // MFMA k-steps per row
   constexpr int CPR = D / 8;  // 16-B chunks per row
   constexpr int SWM = (CPR < 16 ? CPR : 16) - 1;
+  constexpr int GTS = 36;  // s_gt row stride in floats: 16-B rows, conflict-free row reads
   __shared__ uint4 s_prow[kProbes * CPR];  // probe rows, chunk c of row p at p*CPR + (c ^ (p & SWM))
-  __shared__ float s_gt[kProbes][kProbes];  // s_gt[p][b] = cos(probe b, probe p)
+  // s_gt[a*GTS + p] = cos(probe a, probe p) as candidate a's accumulator holds
+  // it (the same rounding the fold applies to a's max term)
+  __shared__ __attribute__((aligned(16))) float s_gt[kProbes * GTS];
   __shared__ float s_pinv[kProbes], s_pscore[kProbes], s_ppen[kProbes];
   __shared__ int s_pcand[kProbes];  // candidate position of each probe slot (-1 = empty)
   __shared__ int s_pitem[kProbes];  // its item id
-  __shared__ int8_t s_slot[kMaxC];  // candidate position -> probe slot (-1 = not a probe)
+  __shared__ int s_citem[kMaxC];    // candidate position -> item id
+  // per-candidate score and 1/|e|, indexed wave-locally: position c at
+  // cidx(c) = (c & 7) * 128 + (c >> 3), i.e. wave w, tile j, lane q at w*128 + 32j + q
+  __shared__ float s_cscore[kMaxC], s_cinv[kMaxC];
   __shared__ uint64_t s_wbound[kWaves];
   __shared__ int s_round[2];  // rounds done, picked probe mask (written by wave 0)
-  // s_sim[p][w*128 + 32j + q] = cos(probe p, candidate cpos(j) of wave w): the
-  // batch's columns, parked in LDS so no accumulator stays live in the rounds
-  __shared__ float s_sim[kProbes * kMaxC];
+  __shared__ int s_out[kMaxC];
+  // the picks, stored to HBM once at the end
+  // Barriers inside the batch loop order LDS only: a raw s_barrier after
+  // lgkmcnt(0), so no wave waits there for its outstanding global stores.
+  auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
   const int64_t u = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, q = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, q = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave index in an SGPR
   const float mu = 1.f - lambda;
   auto cpos = [&](int j) { return kWaves * (32 * j + q) + w; };  // this lane's position in tile j
-
-  for (int i = tid; i < kMaxC; i += kThreads) s_slot[i] = -1;
+  auto cidx = [&](int j) { return w * 128 + 32 * j + q; };      // = (cpos & 7) * 128 + (cpos >> 3)
+#ifdef DR_MMR_DIAG
+  uint64_t dg[kMgSlots] = {};
+#endif
+  MG_T0(t_kernel);
 
   // ---- candidate rows -> B fragments (lane: position cpos(j), k = 16s + 8h .. +7)
   bf16x8 brow[kTiles][KS];
-  float score[kTiles], inv[kTiles], pen[kTiles];
-  int32_t citem[kTiles];
+  float pen[kTiles];  // max cosine to the picks so far (-inf before the first)
   uint32_t live = 0;
+  int nbad = 0;
 #pragma unroll
   for (int j = 0; j < kTiles; ++j) {
     const int c = cpos(j);
-    const int32_t item = c < C ? cand_items[u * C + c] : -1;
+    int32_t item = c < C ? cand_items[u * C + c] : -1;
+    if (item >= 0 && (int64_t)item >= n_items) {  // out of range: counted, never picked
+      nbad += h == 0 ? 1 : 0;
+      item = -1;
+    }
     const bool ok = item >= 0;
-    citem[j] = item;
     live |= (ok ? 1u : 0u) << j;
-    score[j] = ok ? cand_scores[u * C + c] : 0.f;
-    pen[j] = -INFINITY;  // max cosine to the picks so far (none yet)
+    const float sc = ok ? cand_scores[u * C + c] : 0.f;
+    if (h == 0) {
+      s_citem[c] = item;
+      s_cscore[cidx(j)] = sc;
+    }
+    pen[j] = -INFINITY;
     const uint4* src = reinterpret_cast<const uint4*>(E + (int64_t)(ok ? item : 0) * D) + h;
 #pragma unroll
     for (int s = 0; s < KS; ++s) brow[j][s] = __builtin_bit_cast(bf16x8, src[2 * s]);
   }
+  if (nbad && err) atomicAdd(err, nbad);
 #pragma unroll
   for (int j = 0; j < kTiles; ++j) {
     float nsq = 0.f;
@@ -132,135 +207,168 @@ __global__ __launch_bounds__(kThreads) void mmr_probe_kernel(
       }
     }
     nsq += __shfl_xor(nsq, 32);  // the two half-rows of the candidate
-    inv[j] = 1.f / sqrtf(nsq);
+    if (h == 0) s_cinv[cidx(j)] = 1.f / sqrtf(nsq);
   }
   __syncthreads();
+  MG_ADD(kMgLoad, t_kernel);
 
   int t = 0;
   // every batch picks at least once (its best probe beats BOUND by
   // construction), so k_out batches always suffice; the cap only bounds the
   // loop should that invariant ever break
   for (int batch = 0; t < k_out && batch <= k_out; ++batch) {
+    // Lane coordinates re-derived from an opaque copy of the thread id every
+    // batch: otherwise hipcc hoists dozens of per-lane LDS offsets out of the
+    // loop, and with 192 VGPRs of rows + columns resident they spill (and the
+    // reloads land inside the MFMA chain).
+    uint32_t tl = threadIdx.x;
+    asm volatile("" : "+v"(tl));
+    const int lane = (int)(tl & 63u), h = lane >> 5, q = lane & 31;
+    auto cpos = [&](int j) { return kWaves * (32 * j + q) + w; };
+    auto cidx = [&](int j) { return w * 128 + 32 * j + q; };
+    MG_T0(t_sel);
+
     // ---- probes: the kPerWave best live candidates of this wave + its bound.
     // Lane (q, h) ranks tiles 2h and 2h+1 (the two half-waves hold the same
-    // candidates; this way each is counted once).
+    // candidates; this way each is counted once). Key = ord(value) << 32 |
+    // ~position: (value desc, position asc), exact.
     uint64_t kk[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      const float sc = s_cscore[w * 128 + 32 * (2 * h + i) + q];
       uint64_t key = 0ull;
 #pragma unroll
       for (int j = 0; j < kTiles; ++j) {
         if (j == 2 * h + i && ((live >> j) & 1u)) {
-          const float val = lambda * score[j] - mu * (t == 0 ? 0.f : pen[j]);
+          // the value every phase computes: lambda*s before the first pick,
+          // then fma(-mu, pen, lambda*s)
+          const float val = t == 0 ? lambda * sc : fmaf(-mu, pen[j], lambda * sc);
           key = dr::make_key(val, (uint32_t)cpos(j));
         }
       }
       kk[i] = key;
+      (void)sc;
     }
+    int pc[kPerWave];  // positions of this wave's probes (uniform; -1 = none)
+    // per lane: probe slot + 1 of its candidate in tile j at bits 8j .. 8j+7
+    uint32_t myslot = 0u;
 #pragma unroll
     for (int m = 0; m <= kPerWave; ++m) {
-      const uint64_t best = wave_max_u64(dr::umax64(kk[0], kk[1]));
+      const uint64_t lb = dr::umax64(kk[0], kk[1]);  // this lane's best key
+      const uint32_t hi = (uint32_t)(lb >> 32);
+      const uint32_t mh = wmax_u32<64>(hi);  // best value (ord); 0 = no live key left
+      uint64_t best = 0ull;
+      if (mh != 0u) {
+        const uint64_t bal = __ballot(hi == mh);
+        if (__popcll(bal) == 1) best = dr::readlane_u64(lb, __builtin_ctzll(bal));
+        else best = wave_max_u64(hi == mh ? lb : 0ull);  // equal values: lowest position
+      }
       if (m == kPerWave) {
         if (lane == 0) s_wbound[w] = best;
         break;
       }
       const int slot = w * kPerWave + m;
+      pc[m] = __builtin_amdgcn_readfirstlane(best != 0ull ? (int)dr::key_item(best) : -1);
       if (best != 0ull) {
         kk[0] = kk[0] == best ? 0ull : kk[0];
         kk[1] = kk[1] == best ? 0ull : kk[1];
-        if (lane == 0) {
-          const int c = (int)dr::key_item(best);
-          s_slot[c] = (int8_t)slot;
-          s_pcand[slot] = c;
-        }
-      } else if (lane == 0) {
-        s_pcand[slot] = -1;
+        const int pj = (pc[m] >> 3) >> 5, pq = (pc[m] >> 3) & 31;
+        if (q == pq) myslot |= (uint32_t)(slot + 1) << (8 * pj);
       }
+      if (lane == 0) s_pcand[slot] = pc[m];
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // owners stage their probe rows (both half-rows) and per-probe state
+    MG_ADD(kMgSelect, t_sel);
+    MG_T0(t_stage);
+    // the owners of each probe (lanes of its tile column, both halves) stage
+    // its row and state
 #pragma unroll
     for (int j = 0; j < kTiles; ++j) {
-      const int sl = s_slot[cpos(j)];
+      const int sl = (int)((myslot >> (8 * j)) & 255u) - 1;
       if (sl >= 0) {
 #pragma unroll
         for (int s = 0; s < KS; ++s)
           s_prow[sl * CPR + ((2 * s + h) ^ (sl & SWM))] = __builtin_bit_cast(uint4, brow[j][s]);
         if (h == 0) {
-          s_pitem[sl] = citem[j];
-          s_pinv[sl] = inv[j];
-          s_pscore[sl] = score[j];
+          s_pitem[sl] = s_citem[cpos(j)];
+          s_pinv[sl] = s_cinv[cidx(j)];
+          s_pscore[sl] = s_cscore[cidx(j)];
           s_ppen[sl] = pen[j];
         }
       }
     }
-    __syncthreads();
+    MG_T0(t_sbar);
+    lds_barrier();
+    MG_ADD(kMgStageBar, t_sbar);
     uint64_t bound = 0ull;
 #pragma unroll
     for (int i = 0; i < kWaves; ++i) bound = dr::umax64(bound, s_wbound[i]);
+    MG_ADD(kMgStage, t_stage);
+    MG_T0(t_mma);
 
     // ---- MFMA: dot(probe p, candidate) for the 32 probes x this wave's 128
-    // candidates, two tiles at a time (32 accumulator registers, not 64: the
-    // candidate rows already take 4 * KS * 4 VGPRs).
+    // candidates, four independent accumulator chains; the columns stay here
+    // until the fold. Register r of tile j holds probe p(r) = 8*(r/4) + 4h + r%4.
+    f32x16 acc[kTiles];
 #pragma unroll
-    for (int j0 = 0; j0 < kTiles; j0 += 2) {
-      f32x16 acc[2] = {f32x16{}, f32x16{}};
+    for (int j = 0; j < kTiles; ++j) acc[j] = f32x16{};
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const bf16x8 a = __builtin_bit_cast(bf16x8, s_prow[q * CPR + ((2 * s + h) ^ (q & SWM))]);
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 a = __builtin_bit_cast(bf16x8, s_prow[q * CPR + ((2 * s + h) ^ (q & SWM))]);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, brow[j0 + i][s], acc[i], 0, 0, 0);
-      }
-      // cosines: register r holds probe row p(r) = 8*(r/4) + 4h + r%4
+      for (int j = 0; j < kTiles; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, brow[j][s], acc[j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j) {
+      const float ci = s_cinv[cidx(j)];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 v = *reinterpret_cast<const float4*>(&s_pinv[8 * g + 4 * h]);
         const float pv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            acc[i][4 * g + e] = acc[i][4 * g + e] * inv[j0 + i] * pv[e];
-      }
-      // park the columns; the owner of probe b also writes its row of s_gt
-      // (rows 8*(r/4) + r%4 below are immediate LDS offsets)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int j = j0 + i;
-        float* simc = &s_sim[4 * h * kMaxC + w * 128 + 32 * j + q];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) simc[(8 * (r >> 2) + (r & 3)) * kMaxC] = acc[i][r];
-        const int sl = s_slot[cpos(j)];
-        if (sl >= 0) {
-          float* col = &s_gt[4 * h][sl];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) col[(8 * (r >> 2) + (r & 3)) * kProbes] = acc[i][r];
-        }
+        for (int e = 0; e < 4; ++e) acc[j][4 * g + e] = acc[j][4 * g + e] * ci * pv[e];
       }
     }
-    __syncthreads();
+    MG_T0(t_gt);
+    // the owners of probe b write row b of s_gt (their column of the batch)
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j) {
+      const int sl = (int)((myslot >> (8 * j)) & 255u) - 1;
+      if (sl >= 0) {
+        float* row = &s_gt[sl * GTS + 4 * h];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) row[8 * (r >> 2) + (r & 3)] = acc[j][r];
+      }
+    }
+    MG_ADD(kMgGt, t_gt);
+    MG_ADD(kMgMma, t_mma);
+    MG_T0(t_sync1);
+    lds_barrier();
+    MG_ADD(kMgSync1, t_sync1);
+    MG_T0(t_rounds);
 
     // ---- fast rounds over the probes: wave 0 alone (the other waves wait at
     // the batch-end barrier). Lane a < 32 holds probe a. The argmax is a 32-bit
-    // max of ord(value) (DPP); an exact tie of values falls back to the lowest
-    // candidate position, so the pick is the (value desc, position asc) max.
+    // max of ord(value) (fused DPP); an exact tie of values falls back to the
+    // lowest candidate position, so the pick is the (value desc, position asc) max.
     if (w == 0) {
       const int pa = lane < kProbes ? s_pcand[lane] : -1;
       const int pitem = lane < kProbes ? s_pitem[lane] : -1;
-      const float sa = lane < kProbes ? s_pscore[lane] : 0.f;
+      const float lsa = lambda * (lane < kProbes ? s_pscore[lane] : 0.f);
       float pna = lane < kProbes ? s_ppen[lane] : 0.f;
+      const int gbase = (lane & 31) * GTS;
+      const uint32_t bhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bound >> 32));
+      const uint32_t blo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bound);
+      const bool first = t == 0;  // round 0 ranks without the max term: one pick, then a new batch
       bool alive = pa >= 0;
       uint32_t picked = 0;
       while (t < k_out) {
-        const float val = lambda * sa - mu * (t == 0 ? 0.f : pna);
+        const float val = first ? lsa : fmaf(-mu, pna, lsa);
         const uint32_t ov = alive ? dr::f32_to_ord(val) : 0u;  // live ords are > 0
-        const uint32_t m = wave_max_u32_32(ov);
+        const uint32_t m = wmax_u32<32>(ov);
         if (m == 0u) {  // no live probe
-          if (bound != 0ull) break;
-          if (lane == 0) out_items[u * k_out + t] = -1;  // no live candidate left
+          if ((bhi | blo) != 0u) break;
+          if (lane == 0) s_out[t] = -1;  // no live candidate left
           ++t;
           continue;
         }
@@ -270,68 +378,99 @@ __global__ __launch_bounds__(kThreads) void mmr_probe_kernel(
           bal = __ballot(ov == m && (uint32_t)pa == mp);
         }
         const int pk = __builtin_ctzll(bal);
-        const uint32_t pos = (uint32_t)__builtin_amdgcn_readlane(pa, pk);
-        if ((((uint64_t)m << 32) | (uint64_t)~pos) <= bound) break;  // a non-probe may be better
-        if (lane == pk) out_items[u * k_out + t] = pitem;
+        const uint32_t npos = ~(uint32_t)__builtin_amdgcn_readlane(pa, pk);
+        if (m < bhi || (m == bhi && npos <= blo)) break;  // a non-probe may be better
+        const float g = s_gt[gbase + pk];  // issued ahead of the bookkeeping
+        if (lane == pk) s_out[t] = pitem;
         picked |= 1u << pk;
         alive = alive && lane != pk;
-        if (lane < kProbes) pna = fmaxf(pna, s_gt[pk][lane]);
         ++t;
-        if (t == 1) break;  // round 0 ranked without the max term: all values move
+        if (first) break;
+        pna = fmaxf(pna, g);
       }
       if (lane == 0) {
         s_round[0] = t;
         s_round[1] = (int)picked;
       }
     }
-    __syncthreads();
+    MG_ADD(kMgRounds, t_rounds);
+    MG_T0(t_sync2);
+    lds_barrier();
     t = s_round[0];
     const uint32_t picked = (uint32_t)s_round[1];
+    MG_ADD(kMgSync2, t_sync2);
+    MG_T0(t_fold);
 
-    // ---- batch end: fold the picked columns into every candidate's max term
-    for (uint32_t m = picked; m != 0u; m &= m - 1u) {  // wave-uniform
-      const float* simr = &s_sim[__builtin_ctz(m) * kMaxC + w * 128 + q];
-#pragma unroll
-      for (int j = 0; j < kTiles; ++j) pen[j] = fmaxf(pen[j], simr[32 * j]);
-    }
+    // ---- batch end: fold the picked columns into every candidate's max term,
+    // straight from the accumulators (lane half h holds probes 8i + 4h + e)
+    const uint32_t pm = picked >> (4 * h);
 #pragma unroll
     for (int j = 0; j < kTiles; ++j) {
-      const int sl = s_slot[cpos(j)];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if ((pm >> (8 * (r >> 2) + (r & 3))) & 1u) mx = fmaxf(mx, acc[j][r]);
+      pen[j] = fmaxf(pen[j], half_swap_max(mx));
+    }
+    // picked probes of this wave leave the live set
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j) {
+      const int sl = (int)((myslot >> (8 * j)) & 255u) - 1;
       if (sl >= 0 && ((picked >> sl) & 1u)) live &= ~(1u << j);
     }
-    __syncthreads();  // s_prow / s_gt / s_sim / s_wbound are rewritten by the next batch
-#pragma unroll
-    for (int j = 0; j < kTiles; ++j)
-      if (s_slot[cpos(j)] >= 0) s_slot[cpos(j)] = -1;
+    lds_barrier();  // s_prow / s_gt / s_wbound / s_pcand are rewritten by the next batch
+    MG_ADD(kMgFold, t_fold);
+#ifdef DR_MMR_DIAG
+    dg[kMgBatches] += 1;
+#endif
   }
+  __syncthreads();
+  for (int i = tid; i < k_out; i += kThreads) out_items[u * k_out + i] = s_out[i];
+#ifdef DR_MMR_DIAG
+  MG_ADD(kMgTotal, t_kernel);
+  if (lane == 0)
+    for (int i = 0; i < kMgSlots; ++i) atomicAdd(&g_mmr_diag[w][i], (unsigned long long)dg[i]);
+#endif
 }
+
+#ifdef DR_MMR_DIAG
+}  // namespace
+// host: copy (and optionally reset) the per-wave phase totals, [8][16] u64
+extern "C" int dr_mmr_diag_read(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mmr_diag), sizeof(g_mmr_diag)) != hipSuccess) return -1;
+  if (reset) {
+    static unsigned long long zero[kWaves][16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_mmr_diag), zero, sizeof(zero)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+namespace {
+#endif
 
 }  // namespace
 
 extern "C" int dr_mmr_rerank(const int32_t* cand_items, const float* cand_scores, int64_t n_users,
                              int C, const void* item_table, int64_t n_items, int d, int k_out,
-                             float lambda, int32_t* out_items, dr_stream_t stream) {
+                             float lambda, int32_t* out_items, int32_t* err, dr_stream_t stream) {
   DR_CHECK_ARG(C >= 1 && C <= kMaxC, "C must be in [1, 1024]");
   DR_CHECK_ARG(k_out >= 1 && k_out <= C, "k_out must be in [1, C]");
   DR_CHECK_ARG(lambda >= 0.f && lambda <= 1.f, "lambda must be in [0, 1]");
-  (void)n_items;
+  DR_CHECK_ARG(n_items >= 0 && n_items < 0x7fffffffLL, "n_items must be in [0, 2^31)");
   if (n_users == 0) return DR_OK;
   DR_CHECK_ARG(cand_items && cand_scores && item_table && out_items, "null pointer");
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)n_users);
+#define DR_MMR(DD)                                                                            \
+  hipLaunchKernelGGL(mmr_batch_kernel<DD>, grid, dim3(kThreads), 0, s, cand_items, cand_scores, \
+                     C, (const __bf16*)item_table, n_items, k_out, lambda, out_items, err)
   switch (d) {
-    case 64:
-      hipLaunchKernelGGL(mmr_probe_kernel<64>, grid, dim3(kThreads), 0, s, cand_items, cand_scores,
-                         C, (const __bf16*)item_table, k_out, lambda, out_items);
-      break;
-    case 128:
-      hipLaunchKernelGGL(mmr_probe_kernel<128>, grid, dim3(kThreads), 0, s, cand_items,
-                         cand_scores, C, (const __bf16*)item_table, k_out, lambda, out_items);
-      break;
+    case 64: DR_MMR(64); break;
+    case 128: DR_MMR(128); break;
     default:
       dr::set_error("dr_mmr_rerank: d must be 64 or 128");
       return DR_EUNSUPPORTED;
   }
+#undef DR_MMR
   DR_CHECK_LAUNCH();
   return DR_OK;
 }

@@ -56,7 +56,7 @@ SIGNATURES = {
                                   _p, _p, _p, _p, _p]),
     "dr_adam_rows": (_i32, [_p, _p, _p, _p, _i64, _p, _i64, _f64, _f64, _f64, _f64, _i64, _i32,
                             _p]),
-    "dr_mmr_rerank": (_i32, [_p, _p, _i64, _i32, _p, _i64, _i32, _i32, _f32, _p, _p]),
+    "dr_mmr_rerank": (_i32, [_p, _p, _i64, _i32, _p, _i64, _i32, _i32, _f32, _p, _p, _p]),
     "dr_rank_metrics": (_i32, [_p, _i32, _i64, _i32, _p, _p, _p, _p, _p, _p, _p]),
     "dr_catalog_histogram": (_i32, [_p, _i32, _i64, _i32, _i64, _p, _p, _p]),
 }

@@ -440,9 +440,12 @@ def catalog_histogram(recs: torch.Tensor, n_items: int) -> Tuple[torch.Tensor, t
 # --------------------------------------------------------------------------- MMR
 def mmr_rerank(
     cand_items: torch.Tensor, cand_scores: torch.Tensor, item_table: torch.Tensor, k_out: int,
-    lam: float = 0.5,
+    lam: float = 0.5, check: bool = True,
 ) -> torch.Tensor:
-    """Greedy MMR over per-user candidates (int32 [n, C] + fp32 [n, C]) -> int32 [n, k_out]."""
+    """Greedy MMR over per-user candidates (int32 [n, C] + fp32 [n, C]) -> int32 [n, k_out].
+    Candidate ids < 0 are empty slots; with ``check`` an id >= the table's row
+    count raises IndexError after the call (one counter read), as indexing the
+    table would (without it such candidates are silently never picked)."""
     dev = B.require_device(cand_items, cand_scores, item_table)
     _need(cand_items.dtype == torch.int32 and cand_scores.dtype == torch.float32,
           "int32 candidate ids, fp32 scores")
@@ -454,12 +457,14 @@ def mmr_rerank(
     out = torch.empty((n, int(k_out)), dtype=torch.int32, device=dev)
     if n == 0:
         return out
+    err = B.error_counter(dev) if check else None
     rc = B.lib().dr_mmr_rerank(
         cand_items.contiguous().data_ptr(), cand_scores.contiguous().data_ptr(), n, C,
         item_table.contiguous().data_ptr(), item_table.size(0), item_table.size(1), int(k_out),
-        float(lam), out.data_ptr(), B.stream(dev),
+        float(lam), out.data_ptr(), B.ptr(err), B.stream(dev),
     )
     B.check(rc, "dr_mmr_rerank")
+    B.raise_if_out_of_range(err, "dr_mmr_rerank")
     return out
 
 

@@ -243,10 +243,13 @@ int dr_catalog_histogram(const void* recs, int rec_dtype, int64_t n_users, int k
  *   lambda * score_i - (1 - lambda) * max_{j in S} cos(e_i, e_j)
  * (ties -> lowest candidate position). cand_items int32 [n_users, C],
  * cand_scores fp32 [n_users, C], item_table bf16 [*, d]; out int32 [n_users, k_out]
- * (item ids in selection order). C <= 1024, k_out <= C, d in {64, 128}. */
+ * (item ids in selection order). C <= 1024, k_out <= C, d in {64, 128}.
+ * Candidate ids < 0 are empty slots; ids >= n_items are added to *err (int32
+ * device counter, may be NULL) and never picked. A user left without live
+ * candidates gets -1 for the remaining picks. */
 int dr_mmr_rerank(const int32_t* cand_items, const float* cand_scores, int64_t n_users, int C,
                   const void* item_table, int64_t n_items, int d, int k_out, float lambda,
-                  int32_t* out_items, dr_stream_t stream);
+                  int32_t* out_items, int32_t* err, dr_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -689,3 +689,23 @@ def test_pri_avg_rank_matches_reference_formula():
     ref_avg = np.array([sum(ranks[i]) / len(ranks[i]) for i in ref_items], dtype=np.float32)
     assert np.array_equal(items.cpu().numpy(), ref_items)
     assert np.array_equal(avg.cpu().numpy(), ref_avg)
+
+
+def test_mmr_rerank_out_of_range_raises():
+    """A candidate id past the table raises IndexError (as indexing it
+    would); with check=False it is skipped like an empty slot."""
+    rng = np.random.default_rng(9)
+    d, ni, n, C, kout = 128, 2000, 4, 64, 10
+    E = oracle.as_bf16_f32(rng.standard_normal((ni, d)).astype(np.float32))
+    cand = np.stack([rng.choice(ni, C, replace=False) for _ in range(n)]).astype(np.int32)
+    sc = rng.standard_normal((n, C)).astype(np.float32)
+    bad = cand.copy()
+    bad[2, 7] = ni + 5
+    args = (torch.from_numpy(bad).to(DEV), torch.from_numpy(sc).to(DEV), _bf16(E), kout, 0.5)
+    with pytest.raises(IndexError):
+        ops.mmr_rerank(*args)
+    got = ops.mmr_rerank(*args, check=False).cpu().numpy()
+    skip = bad.copy()
+    skip[2, 7] = -1
+    assert _mmr_check_positions(got, skip, sc, E, 0.5, tol=1e-4) == 0
+    assert not (got == ni + 5).any()

@@ -61,7 +61,7 @@ def test_argument_errors_without_gpu():
     assert rc == -1 and b"k_out must be <= 1024" in lib.dr_last_error()
     rc = lib.dr_topk_merge(None, None, 3, 10, 1000, 10, None, None, None)
     assert rc == -1 and b"null pointer" in lib.dr_last_error()  # 3 x 1000 > 2048 is accepted
-    rc = lib.dr_mmr_rerank(None, None, 4, 2000, None, 10, 128, 10, 0.5, None, None)
+    rc = lib.dr_mmr_rerank(None, None, 4, 2000, None, 10, 128, 10, 0.5, None, None, None)
     assert rc == -1 and b"C must be" in lib.dr_last_error()
     # empty inputs are a no-op success
     assert lib.dr_gather_dot(None, 0, None, 0, 0, 64, None, None, 0, None, None, None) == 0

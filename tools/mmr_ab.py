@@ -23,13 +23,23 @@ def main():
     ap.add_argument("--users", type=int, default=262144)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--lam", type=float, default=0.5)
+    ap.add_argument("--real", action="store_true",
+                    help="candidates = the real top-C lists of random users (dr_score_topk)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(1)
     n_items, d, C, kout = 10_000_000, 128, 1000, 100
     items = (torch.randn(n_items, d, generator=g, device=dev) / d ** 0.5).to(torch.bfloat16)
-    cand = torch.randint(0, n_items, (args.users, C), generator=g, device=dev, dtype=torch.int32)
-    sc = torch.sort(torch.rand(args.users, C, generator=g, device=dev), dim=1, descending=True).values
+    if args.real:
+        from divrec import ops
+
+        users = (torch.randn(args.users, d, generator=g, device=dev) / d ** 0.5).to(torch.bfloat16)
+        sc, cand = ops.score_topk(users, items, C)
+        del users
+    else:
+        cand = torch.randint(0, n_items, (args.users, C), generator=g, device=dev, dtype=torch.int32)
+        sc = torch.sort(torch.rand(args.users, C, generator=g, device=dev), dim=1,
+                        descending=True).values
     tags = args.libs.split(",")
     libs = {t: lib_for(t) for t in tags}
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -40,7 +50,7 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rc = libs[t].dr_mmr_rerank(cand.data_ptr(), sc.data_ptr(), args.users, C, items.data_ptr(),
-                                   n_items, d, kout, args.lam, out.data_ptr(), stream)
+                                   n_items, d, kout, args.lam, out.data_ptr(), None, stream)
         e1.record()
         assert rc == 0, libs[t].dr_last_error()
         torch.cuda.synchronize()
@@ -52,7 +62,8 @@ def main():
         for t in tags:
             times[t].append(run(t)[0])
         print(f"round {r}: " + " ".join(f"{t}={times[t][-1]:.1f}ms" for t in tags), file=sys.stderr, flush=True)
-    res = {"users": args.users, "lam": args.lam, "variants": {}}
+    res = {"users": args.users, "lam": args.lam, "candidates": "real top-C" if args.real else "random",
+           "variants": {}}
     for t in tags:
         med = statistics.median(times[t])
         res["variants"][t] = {"median_ms": med, "users_per_s": args.users / med * 1e3,

@@ -47,7 +47,7 @@ def lib_for(tag):
     sigs = dict(B.SIGNATURES)
     if tag.startswith("abi1"):
         sigs.update(_ABI1)
-    for fn in ("dr_score_topk_workspace", "dr_score_topk", "dr_last_error"):
+    for fn in ("dr_score_topk_workspace", "dr_score_topk", "dr_last_error", "dr_mmr_rerank"):
         res, args = sigs[fn]
         f = getattr(lib, fn)
         f.restype, f.argtypes = res, args
