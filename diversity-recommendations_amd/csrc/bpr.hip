@@ -13,6 +13,7 @@
 // float atomics); 16-B-per-lane chunks would scatter each atomic instruction
 // over 16-B strides. Any d <= 512. Out-of-range ids are range-checked
 // (include/divrec_hip.h): such a triple reads and adds nothing.
+#include <algorithm>
 #include <cmath>
 
 #include "common.h"
@@ -40,14 +41,47 @@ template <int E>  // row elements per lane: ceil(d / 32)
 __global__ __launch_bounds__(kBlock) void bpr_kernel(
     const float* __restrict__ U, int64_t nu, const float* __restrict__ I, int64_t ni, int64_t d,
     const int64_t* __restrict__ uid, const int64_t* __restrict__ pid,
-    const int64_t* __restrict__ nid, int64_t batch, float grad_scale, float* __restrict__ loss,
-    int32_t* __restrict__ hit, float* __restrict__ gU, float* __restrict__ gI,
-    int32_t* __restrict__ err) {
+    const int64_t* __restrict__ nid, int64_t batch, int64_t span, float grad_scale,
+    float* __restrict__ loss, int32_t* __restrict__ hit, float* __restrict__ gU,
+    float* __restrict__ gI, int32_t* __restrict__ err) {
+  // Each 32-lane group walks a CONTIGUOUS span of triples and keeps one run
+  // per table side: the current user, positive and negative rows are read
+  // once per run of equal ids, and their gradient contributions are summed in
+  // registers and added with ONE row of atomics when the run ends. The
+  // reference's own batches are such runs (PairWiseDataset's m x m product:
+  // one user for m*m triples, each positive repeated m times in a row,
+  // base_datasets.py:94-107), so the atomics per triple drop from 3 rows to
+  // ~1 there; uniform random triples (runs of 1) cost what they did.
   const int gl = threadIdx.x & 31;
   const int64_t group = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 5;
-  const int64_t ngroups = (int64_t)gridDim.x * kBlock / 32;
+  const int64_t b0 = group * span;
+  const int64_t b1 = b0 + span < batch ? b0 + span : batch;
   int bad = 0;
-  for (int64_t b = group; b < batch; b += ngroups) {
+  int64_t cu = -1, cp = -1, cn = -1;  // ids of the current runs (-1 = none)
+  float uv[E], pv[E], nv[E];          // their rows
+  float gu[E], gp[E], gn[E];          // their summed gradient contributions
+#pragma unroll
+  for (int e = 0; e < E; ++e) gu[e] = gp[e] = gn[e] = 0.f;
+  auto load = [&](const float* tab, int64_t r, float (&v)[E]) {
+    const float* row = tab + r * d;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t x = e * 32 + gl;
+      v[e] = x < d ? row[x] : 0.f;
+    }
+  };
+  auto flush = [&](float* g, int64_t r, float (&acc)[E]) {  // one row of atomics
+    if (g && r >= 0) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int64_t x = e * 32 + gl;
+        if (x < d) atomicAdd(g + r * d + x, acc[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = 0.f;
+  };
+  for (int64_t b = b0; b < b1; ++b) {
     const int64_t u = uid[b], p = pid[b], n = nid[b];
     if (!in_rows(u, nu) || !in_rows(p, ni) || !in_rows(n, ni)) {  // uniform in the group
       if (gl == 0) {
@@ -57,17 +91,20 @@ __global__ __launch_bounds__(kBlock) void bpr_kernel(
       }
       continue;
     }
-    const float* ur = U + u * d;
-    const float* pr = I + p * d;
-    const float* nr = I + n * d;
-    float uv[E], pv[E], nv[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int64_t x = e * 32 + gl;
-      const bool ok = x < d;
-      uv[e] = ok ? ur[x] : 0.f;
-      pv[e] = ok ? pr[x] : 0.f;
-      nv[e] = ok ? nr[x] : 0.f;
+    if (u != cu) {
+      flush(gU, cu, gu);
+      cu = u;
+      load(U, u, uv);
+    }
+    if (p != cp) {
+      flush(gI, cp, gp);
+      cp = p;
+      load(I, p, pv);
+    }
+    if (n != cn) {
+      flush(gI, cn, gn);
+      cn = n;
+      load(I, n, nv);
     }
     float sp = 0.f, sn = 0.f;
 #pragma unroll
@@ -88,16 +125,14 @@ __global__ __launch_bounds__(kBlock) void bpr_kernel(
     const float g = neg_log_sigmoid_grad(x) * grad_scale;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int64_t x2 = e * 32 + gl;
-      if (x2 < d) {
-        if (gU) atomicAdd(gU + u * d + x2, g * pv[e] - g * nv[e]);
-        if (gI) {
-          atomicAdd(gI + p * d + x2, g * uv[e]);
-          atomicAdd(gI + n * d + x2, -g * uv[e]);
-        }
-      }
+      gu[e] += g * pv[e] - g * nv[e];
+      gp[e] += g * uv[e];
+      gn[e] += -g * uv[e];
     }
   }
+  flush(gU, cu, gu);
+  flush(gI, cp, gp);
+  flush(gI, cn, gn);
   if (bad && err) atomicAdd(err, bad);
 }
 
@@ -196,12 +231,15 @@ extern "C" int dr_bpr_fwd_bwd(const float* user_table, int64_t n_user_rows,
   DR_CHECK_ARG(user_table && item_table && user_id && pos_id && neg_id, "null pointer");
   DR_CHECK_ARG(d >= 1 && d <= 512, "d must be in [1, 512]");
   hipStream_t s = (hipStream_t)stream;
-  int64_t grid = dr::ceil_div(batch, kBlock / 32);
-  if (grid > 256 * 8) grid = 256 * 8;  // grid-stride the rest
+  // contiguous spans of triples per 32-lane group, up to 8 workgroups per CU
+  constexpr int64_t kGroups = 256 * 8 * (kBlock / 32);
+  // (at least 16 per span, so runs are summed in small batches too)
+  const int64_t span = std::max<int64_t>(16, dr::ceil_div(batch, kGroups));
+  const int64_t grid = dr::ceil_div(dr::ceil_div(batch, span), kBlock / 32);
 #define DR_BPR(EE)                                                                          \
   hipLaunchKernelGGL(bpr_kernel<EE>, dim3((unsigned)grid), dim3(kBlock), 0, s, user_table,  \
                      n_user_rows, item_table, n_item_rows, d, user_id, pos_id, neg_id, batch, \
-                     grad_scale, loss, hit, grad_user, grad_item, err)
+                     span, grad_scale, loss, hit, grad_user, grad_item, err)
   switch ((int)dr::ceil_div(d, 32)) {
     case 1: DR_BPR(1); break;
     case 2: DR_BPR(2); break;

@@ -709,3 +709,48 @@ def test_mmr_rerank_out_of_range_raises():
     skip[2, 7] = -1
     assert _mmr_check_positions(got, skip, sc, E, 0.5, tol=1e-4) == 0
     assert not (got == ni + 5).any()
+
+
+@pytest.mark.parametrize("d", [100, 128])
+def test_bpr_fwd_bwd_mxm_runs(d):
+    """The reference's triple layout (PairWiseDataset: users in order, m*m
+    triples each, each positive repeated m times in a row, the negatives
+    cycled): runs of equal ids are summed in registers before the atomics.
+    Gradients against the oracle, with an out-of-range id inside a run."""
+    rng = np.random.default_rng(16)
+    nu, ni, m, n_users = 50, 400, 20, 45
+    U = rng.standard_normal((nu, d)).astype(np.float32) * 0.3
+    I = rng.standard_normal((ni, d)).astype(np.float32) * 0.3
+    users = rng.choice(nu, n_users)
+    pos = rng.integers(0, ni, (n_users, m))
+    neg = rng.integers(0, ni, (n_users, m))
+    uid = np.repeat(users, m * m)
+    pid = np.repeat(pos, m, axis=1).reshape(-1)
+    nid = np.tile(neg, (1, m)).reshape(-1)
+    B = uid.size
+    gU = torch.zeros(nu, d, device=DEV)
+    gI = torch.zeros(ni, d, device=DEV)
+    loss, hit = ops.bpr_fwd_bwd(torch.from_numpy(U).to(DEV), torch.from_numpy(I).to(DEV),
+                                torch.from_numpy(uid).to(DEV), torch.from_numpy(pid).to(DEV),
+                                torch.from_numpy(nid).to(DEV), 1.0 / B, gU, gI)
+    rl, ra, rU, rI = oracle.bpr_forward_backward(U, I, uid, pid, nid)
+    assert abs(loss.double().mean().item() - rl) <= 1e-5 * abs(rl)
+    assert abs(hit.double().mean().item() - ra) <= 1.0 / B
+    assert np.allclose(gU.cpu().numpy(), rU, rtol=1e-4, atol=1e-7)
+    assert np.allclose(gI.cpu().numpy(), rI, rtol=1e-4, atol=1e-7)
+    # an invalid positive in the middle of a run: that triple adds nothing, raises
+    bad = pid.copy()
+    bad[5 * m * m + 7] = ni + 3
+    gU.zero_()
+    gI.zero_()
+    with pytest.raises(IndexError):
+        ops.bpr_fwd_bwd(torch.from_numpy(U).to(DEV), torch.from_numpy(I).to(DEV),
+                        torch.from_numpy(uid).to(DEV), torch.from_numpy(bad).to(DEV),
+                        torch.from_numpy(nid).to(DEV), 1.0 / B, gU, gI)
+    keep = np.ones(B, dtype=bool)
+    keep[5 * m * m + 7] = False
+    _, _, rU2, rI2 = oracle.bpr_forward_backward(U, I, uid[keep], pid[keep], nid[keep])
+    # the oracle averages over its own batch size: rescale to 1/B
+    sc = keep.sum() / B
+    assert np.allclose(gU.cpu().numpy(), rU2 * sc, rtol=1e-4, atol=1e-7)
+    assert np.allclose(gI.cpu().numpy(), rI2 * sc, rtol=1e-4, atol=1e-7)
