@@ -85,7 +85,7 @@ def parse():
                     help="after timing, recompute this many of each rank's final users "
                          "over the whole catalog on one device and require identical lists")
     ap.add_argument("--workload", default="catalog",
-                    choices=["catalog", "score1m", "gather", "bpr", "mmr", "fp32"])
+                    choices=["catalog", "score1m", "gather", "bpr", "mmr", "fp32", "ml100k"])
     ap.add_argument("--candidates", type=int, default=1000, help="mmr: top-C candidates per user")
     ap.add_argument("--mmr-k", type=int, default=100, help="mmr: re-ranked list length")
     ap.add_argument("--mmr-lambda", type=float, default=0.5)
@@ -558,6 +558,9 @@ def secondary(args):
                "kernel": "dr_score_topk (sample scan + thresholds + seeded scan + finalize)"}, cpu)
         return 0
 
+    if args.workload == "ml100k":
+        return ml100k(args, dev, g)
+
     if args.workload == "fp32":
         # MatrixFactorization.score_topk's default (fp32-faithful) mode on the
         # reference experiments' own width, d = 100 (zero-padded to 128 once
@@ -813,6 +816,92 @@ def secondary(args):
         return 0
 
     raise ValueError(args.workload)
+
+
+def ml100k(args, dev, g):
+    """configs[0]: the reference's evaluation step on an ML-100K-shaped
+    synthetic set (943 users, 1682 items, ~90.5k train + 10 test interactions
+    per user, MatrixFactorization d=32) through the drop-in API:
+    recommendations_score_loop = get_model_recommendations (top-10, frozen =
+    train items, fp32 scoring) + cosine ILD (the reference's dense D) +
+    P@10 / R@10 / MAP@10 / NDCG@10 + Entropy + PRI. The reference runs this on
+    the CPU; here the model lives on the GPU (there is no CPU compute path),
+    so the line is the whole step's wall time with host-side datasets, as a
+    user of the reference would call it. The CPU baseline is the reference
+    loop restated in torch (oracle.reference_loop_topk + oracle.ild_sequential)."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "diversity-recommendations_amd"))
+    from divrec import datasets, losses, metrics, models, train
+
+    nu, ni, d, k = 943, 1682, 32, 10
+    rng = np.random.default_rng(100)
+    tr, te = [], []
+    for u in range(nu):  # ~96 train + 10 test items per user, disjoint
+        its = rng.choice(ni, 106, replace=False)
+        tr += [(u, int(i)) for i in its[10:]]
+        te += [(u, int(i)) for i in its[:10]]
+    tr_t, te_t = torch.tensor(tr, dtype=torch.int64), torch.tensor(te, dtype=torch.int64)
+    train_ds = datasets.UserItemInteractionsDataset(tr_t, number_of_users=nu, number_of_items=ni)
+    test_ds = datasets.UserItemInteractionsDataset(te_t, number_of_users=nu, number_of_items=ni)
+    full = datasets.UserItemInteractionsDataset(torch.cat([tr_t, te_t]), number_of_users=nu,
+                                                number_of_items=ni)
+    rds = datasets.RankingDataset(test_ds, frozen=train_ds)
+    mf = models.MatrixFactorization(nu, ni, d)  # N(0, 1) fp32 init, as the reference
+    It = mf.item_embeddings.weight.detach().clone()
+    En = It / It.norm(dim=1, keepdim=True)
+    Dc = 1.0 - En @ En.T  # the reference's dense cosine distance matrix
+    mf = mf.to(dev)
+    scores = [losses.IntraListDiversityScore(distance_matrix=Dc, reduction="none"),
+              metrics.PrecisionAtKScore(), metrics.RecallAtKScore(),
+              metrics.MeanAveragePrecisionAtKScore(), metrics.NDCGScore(),
+              metrics.EntropyDiversityScore(dataset=full), metrics.PRI(dataset=full)]
+
+    def step():
+        return train.recommendations_score_loop(rds, mf, scores, k)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / args.steps
+    cpu = None
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        import oracle
+
+        threads, visible, model = host_cpu()
+        torch.set_num_threads(threads)
+        Uh, Ih = mf.user_embeddings.weight.detach().cpu(), It
+        frozen = [tr_t[tr_t[:, 0] == u, 1].tolist() for u in range(nu)]
+        t0 = time.perf_counter()
+        recs = oracle.reference_loop_topk(Uh, Ih, k, users=list(range(nu)), frozen=frozen)
+        oracle.ild_sequential(recs.numpy(), Dc.numpy())
+        t = time.perf_counter() - t0
+        cpu = {"value": nu / t, "unit": "users/s (top-10 + ILD)", "cores": threads, "kind": "port",
+               "cpu_model": model, "cpus_visible": visible,
+               "sample": f"oracle.reference_loop_topk (the reference get_model_recommendations loop "
+                         f"restated in torch) + oracle.ild_sequential (the combinations-order fp32 "
+                         f"sum) over all {nu} users, {t:.2f}s on {threads} threads"}
+    names = ["ild", "precision", "recall", "map", "ndcg", "entropy", "pri"]
+    vals = {n: float(r.float().mean()) if r.dim() else float(r) for n, r in zip(names, res)}
+    rec = {"metric": "config 1 evaluation users/sec: ML-100K-shaped MF d=32 top-10 + ILD + 6 metrics "
+                     "(BASELINE configs[0])",
+           "value": nu / wall, "unit": "users/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": wall * 1e3, "higher_is_better": True,
+           "scaling": "replicas", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic ML-100K-shaped interactions (seeded), N(0,1) fp32 MF weights",
+           "config": {"workload": "recommendations_score_loop: get_model_recommendations top-10 "
+                                  "(frozen = train) + cosine ILD + P/R/MAP/NDCG@10 + Entropy + PRI",
+                      "users": nu, "items": ni, "dim": d, "k": k},
+           "roofline": None, "cpu_baseline": cpu, "metric_values": vals,
+           "note": "host-side datasets and metric plumbing dominate at this size; the reference "
+                   "config runs on the CPU, this build has no CPU compute path (DESIGN.md §1)"}
+    print(json.dumps(rec), flush=True)
+    return 0
 
 
 def mmr_pipeline(args):

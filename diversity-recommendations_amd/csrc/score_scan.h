@@ -101,6 +101,9 @@ enum {
 #ifndef DR_STAGE_BLOCKS
 #define DR_STAGE_BLOCKS 64  // staged lane blocks per wave (>= 64: one user tile always fits)
 #endif
+#ifndef DR_RESOLVE_BATCHED
+#define DR_RESOLVE_BATCHED 1  // staged blocks: one LDS slot reservation per block, not per score
+#endif
 #ifndef DR_COMPACT_INLINE
 #define DR_COMPACT_INLINE __noinline__
 #endif
@@ -847,7 +850,10 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
     // parallel across blocks, off the MFMA loop. A block's threshold is the one
     // at staging time: thresholds only rise, so it admits a superset.
     int nblk = 0;  // staged blocks (wave-uniform)
-    auto resolve = [&]() {
+    // BATCHED: the stage-end form (accumulators dead there); the in-loop
+    // overflow call keeps the light per-score form, whose few registers fit
+    // beside the live accumulators
+    auto resolve = [&](auto BATCHED) {
       DG_T0(t_d);
       wave_lds_sync();
 #pragma unroll 1
@@ -863,6 +869,48 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         const int vld = live ? (int)(info >> 17) : 0;
         uint64_t* ubuf = cbase + (size_t)slot * CAP;
         const float4* src = reinterpret_cast<const float4*>(blk_val + ii * 16);
+        if constexpr (decltype(BATCHED)::value != 0) {
+        // One pass over the block's 16 scores builds the survivor mask and
+        // keeps the survivor's value and row (the common case is one); ONE
+        // LDS atomic per block then reserves all its slots. The per-score
+        // atomics this replaces were a serial chain of LDS round trips.
+        uint32_t mask = 0u;
+        float hv = 0.f;
+        int hr = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v4 = src[q];
+          const float vq[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = j + 8 * q + 4 * hh;  // score register r = 4q + j
+            const bool hit = row < vld && vq[j] > th;
+            mask |= (hit ? 1u : 0u) << (4 * q + j);
+            hv = hit ? vq[j] : hv;
+            hr = hit ? row : hr;
+          }
+        }
+        const uint32_t n = (uint32_t)__popc(mask);
+        uint32_t pos = 0u;
+        if (n) pos = atomicAdd(&ucnt[slot], n);
+        // pos + n <= CAP always holds (flush_at + MARGIN <= CAP); the tests
+        // keep a broken invariant from ever writing past the buffer
+        if (n == 1u && pos < (uint32_t)CAP) st64(ubuf + pos, dr::make_key(hv, gb + (uint32_t)hr));
+        if (__ballot(n == 1u) != 0ull) vmc += 1;
+        // blocks with several survivors (rare): one store per survivor
+        uint32_t rest = n > 1u ? mask : 0u;
+        while (__ballot(rest != 0u) != 0ull) {
+          if (rest != 0u) {
+            const int r = __builtin_ctz(rest);
+            rest &= rest - 1u;
+            const float v = blk_val[ii * 16 + r];
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (pos < (uint32_t)CAP) st64(ubuf + pos, dr::make_key(v, gb + (uint32_t)row));
+            ++pos;
+          }
+          vmc += 1;  // one store instruction (some lane had a key)
+        }
+        } else {
         // four registers (one float4) at a time: few VGPRs, so this also runs
         // inside stage_hits with the accumulators live
 #pragma unroll 1
@@ -883,6 +931,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
               vmc += 1;  // one store instruction (some lane had a key)
             }
           }
+        }
         }
       }
       nblk = 0;
@@ -906,7 +955,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         const uint64_t bal = __ballot(hit);
         if (bal == 0ull) continue;
         const int n = __popcll(bal);
-        if (nblk + n > SB) resolve();  // rare (a scan's first stages): few registers
+        if (nblk + n > SB) resolve(IC<0>{});  // rare (a scan's first stages): few registers
         if (hit) {
           const int i = nblk + lane_prefix(bal);
           float4* dst = reinterpret_cast<float4*>(blk_val + i * 16);
@@ -935,7 +984,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         if (hit_bits != 0u) stage_hits(t, acc, hit_bits, GI);
         // end of a stage: resolve the staged blocks, compact full buffers
         if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) {
-          if (nblk > 0) resolve();
+          if (nblk > 0) resolve(IC<DR_RESOLVE_BATCHED>{});
           check_compact();
         }
       } else {
