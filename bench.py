@@ -408,7 +408,11 @@ def main():
         "ild_roofline": dict(_hbm(U_n // world * (k * 8 + k * d * 2 + 4), r["ild_max"],
                                   pmc_traffic("catalog", cfg_key, "ild_embedding_regs")),
                              kernel="dr_ild_embedding (cosine)",
-                             per_unit=f"{k * 8 + k * d * 2 + 4} B/user = k ids + k bf16 rows + out"),
+                             per_unit=f"{k * 8 + k * d * 2 + 4} B/user = k ids + k bf16 rows + out",
+                             # at k=100 report the MFMA side too (upper-triangle Gram)
+                             mfma_tflops=U_n // world * k * (k - 1) * d / r["ild_max"] / 1e12,
+                             mfma_frac=U_n // world * k * (k - 1) * d / r["ild_max"] / 1e12
+                             / MFMA_BF16_PEAK_TFLOPS),
         "score_topk_ms": r["topk_s"] * 1e3,
         "score_topk_ms_max_over_ranks": r["topk_max"] * 1e3,
         "ild_ms": r["ild_max"] * 1e3,
