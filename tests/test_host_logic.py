@@ -115,3 +115,77 @@ def test_device_pairwise_dataset_csr_and_no_cpu_fallback():
         next(iter(ds.loader(batch_size=8)))
     with pytest.raises(ValueError):
         DevicePairWiseDataset(data, max_sampled=0, device="cpu")
+
+
+def test_user_item_csr_matches_unique_rows():
+    """user_item_csr (1-D key unique) == torch.unique(dim=0) order, with
+    duplicates, users past n_users and an empty user."""
+    rng = np.random.default_rng(3)
+    inter = torch.from_numpy(np.stack([rng.integers(0, 60, 3000), rng.integers(0, 500, 3000)], 1))
+    inter = torch.cat([inter, inter[:200], torch.LongTensor([[70, 1], [5, 499]])])
+    ds = UserItemInteractionsDataset(inter, number_of_users=80, number_of_items=500)
+    rowptr, items = ds.user_item_csr(65)
+    ref = torch.unique(inter, dim=0)
+    ref = ref[ref[:, 0] < 65]
+    assert rowptr.numel() == 66 and int(rowptr[-1]) == ref.shape[0]
+    assert torch.equal(items.to(torch.int64), ref[:, 1])
+    counts = torch.bincount(ref[:, 0], minlength=65)
+    assert torch.equal(rowptr[1:] - rowptr[:-1], counts)
+
+
+def test_pmc_summaries_feed_bench_traffic(tmp_path):
+    """tools/pmc_kernels.py reduces per-dispatch FETCH/WRITE rows of our
+    kernels only (x2 on FETCH, KB -> B); bench.pmc_traffic groups them by
+    workload phase and sums instantiations of one kernel."""
+    import csv
+    import importlib.util
+    import json
+
+    root = os.path.dirname(os.path.dirname(__file__))
+    spec = importlib.util.spec_from_file_location("pmc_kernels",
+                                                  os.path.join(root, "tools", "pmc_kernels.py"))
+    pk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(pk)
+    assert pk.short_name("void dr_topk::score_scan_kernel<128, 512, false, false>(dr_topk::TopkArgs)") \
+        == "score_scan_kernel<128,512,false,false>"
+    assert pk.short_name("void (anonymous namespace)::adam_kernel(float*, float const*)") == "adam_kernel"
+    fields = ["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"]
+    rows = [(1, "void (anonymous namespace)::bpr_kernel<4>(float const*)", 10.0),
+            (2, "void at::native::(anonymous namespace)::foo<float>(int)", 99.0),
+            (3, "void (anonymous namespace)::bpr_kernel<4>(float const*)", 20.0),
+            (4, "void (anonymous namespace)::bpr_kernel<4>(float const*)", 30.0),
+            (5, "void (anonymous namespace)::bpr_kernel<4>(float const*)", 40.0)]
+    for name, counter, scale in (("f.csv", "FETCH_SIZE", 1.0), ("w.csv", "WRITE_SIZE", 0.5)):
+        with open(tmp_path / name, "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=fields)
+            w.writeheader()
+            for d, k, v in rows:
+                w.writerow({"Dispatch_Id": d, "Kernel_Name": k, "Counter_Name": counter,
+                            "Counter_Value": v * scale})
+    out = tmp_path / "pmc_bpr.json"
+    import sys
+    argv = sys.argv
+    sys.argv = ["pmc_kernels.py", str(tmp_path / "f.csv"), str(tmp_path / "w.csv"), "--workload",
+                "bpr", "--reps", "2", "--config", "bpr", "--out", str(out)]
+    try:
+        pk.main()
+    finally:
+        sys.argv = argv
+    rec = json.load(open(out))
+    assert list(rec["kernels"]) == ["bpr_kernel<4>"]  # the torch kernel is dropped
+    hb = rec["kernels"]["bpr_kernel<4>"]["hbm_bytes"]
+    assert hb == [1024.0 * (2 * v + 0.5 * v) for v in (10.0, 20.0, 30.0, 40.0)]
+    # bench.py: phase groups of `reps` dispatches, averaged per call
+    import shutil
+
+    bench_spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(bench_spec)
+    bench_spec.loader.exec_module(bench)
+    (tmp_path / "profiles").mkdir()
+    shutil.copy(out, tmp_path / "profiles" / "pmc_bpr.json")
+    bench.ROOT = str(tmp_path)
+    assert bench.pmc_traffic("bpr", "bpr", "bpr_kernel", group=0) == (hb[0] + hb[1]) / 2
+    assert bench.pmc_traffic("bpr", "bpr", "bpr_kernel", group=1) == (hb[2] + hb[3]) / 2
+    assert bench.pmc_traffic("bpr", "bpr", "bpr_kernel", per_step=2) == sum(hb) / 2
+    assert bench.pmc_traffic("bpr", "other-config", "bpr_kernel") is None
+    assert bench.pmc_traffic("bpr", "bpr", "bpr_kernel", group=2) is None
