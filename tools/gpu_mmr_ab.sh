@@ -5,4 +5,4 @@ mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "mmr" > gpurun_out/mmr_tests.log 2>&1
 timeout -k 10 300 python tools/mmr_ab.py --libs product --users 262144 > gpurun_out/mmr_ab_rand.json 2> gpurun_out/mmr_ab_rand.err
 timeout -k 10 300 python tools/mmr_ab.py --libs product --users 262144 --real > gpurun_out/mmr_ab_real.json 2> gpurun_out/mmr_ab_real.err
-timeout -k 10 300 python bench.py --workload fp32 > gpurun_out/wl_fp32.json 2> gpurun_out/wl_fp32.err
+timeout -k 10 300 python tools/mmr_diag.py --users 65536 --real > gpurun_out/mmr_diag_real.json 2> gpurun_out/mmr_diag_real.err
