@@ -1,6 +1,7 @@
 #!/bin/bash
-# End-of-round artifacts: parity suite, smoke, headline bench, its rocprof
-# kernel summary, and the secondary workload lines.
+# End-of-session GPU pass: parity suite, smoke, headline bench with its CPU
+# baseline, rocprofv3 kernel summary of the headline, every secondary line,
+# and the PMC passes of the kernels changed this round (BPR, MMR).
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -10,6 +11,7 @@ timeout -k 10 400 python bench.py > gpurun_out/f_bench.log 2>&1
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/f_prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/f_prof.log 2>&1
 cd $GRAFT_REPO_ROOT
-for w in score1m gather bpr mmr; do
-  timeout -k 10 300 python bench.py --workload $w > gpurun_out/f_$w.json 2>> gpurun_out/f_wl.err
+for w in score1m gather bpr mmr fp32 ml100k; do
+  timeout -k 10 300 python bench.py --workload $w > gpurun_out/f_wl_$w.json 2> gpurun_out/f_wl_$w.err
 done
+bash tools/gpu_pmc_kernels.sh bpr mmr
