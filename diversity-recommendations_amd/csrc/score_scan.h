@@ -204,6 +204,13 @@ __device__ __forceinline__ void wait_vmcnt_dyn(int n) {
   else wait_vmcnt<0>();
 }
 
+// Wave-uniform 64-bit value, forced into SGPRs.
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // Issue the LDS-DMA of one stage: rows [row0, row0 + SR*32) of the slice into
 // the ring slot at LDS byte address `lds_stage`. The image is lane-linear
 // (glds writes base + lane*16); the swizzle is on the SOURCE address
@@ -223,7 +230,8 @@ __device__ __forceinline__ void issue_stage(const char* __restrict__ I, int64_t 
   asm volatile("" : "+v"(tid));
   const int lane = (int)(tid & 63u);
   const int wave = (int)(__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
-  const char* base = I + row0 * (2 * D);
+  // readfirstlane: the base is wave-uniform; the asm takes it as an SGPR pair
+  const char* base = reinterpret_cast<const char*>(uni64((int64_t)(I + row0 * (2 * D))));
   const int64_t left = n_items - 1 - row0;
   const int rmax = left < ROWS - 1 ? (int)left : ROWS - 1;
 #pragma unroll
@@ -532,17 +540,26 @@ struct TopkArgs {
   int k;
   const int64_t* excl_rowptr;
   const int32_t* excl_items;
-  int n_chunks;
-  int64_t chunk_items;  // multiple of the stage's item count
+  // Units (one workgroup pass each; DESIGN.md §3.1 "grid tail"): the first
+  // n_head user blocks scan the whole catalog in one unit; each of the other
+  // n_ublocks - n_head ("tail") blocks is split into tail_chunks catalog chunks
+  // of chunk_items rows, so the last round of a grid of whole-catalog units
+  // does not leave CUs idle. Chunk 0 of every block uses the user's buffer
+  // row = its position; chunk j >= 1 of tail block b uses row n_users_pad +
+  // ((j - 1) * n_tail + b - n_head) * UPWG + (position within the block).
   int64_t n_ublocks;
+  int64_t n_head;
+  int tail_chunks;
+  int64_t chunk_items;  // multiple of the stage's item count
+  int end_keep;         // tail chunk units compact buffers above this count at their end
   const float* init_thr;  // [n_users_pad] starting thresholds (SEEDED scans only)
   // Fallback rescan only: the user count lives on the device (n_users and
   // n_ublocks above are its upper bounds), and pos_map[p] is the caller's
   // position of list entry p (its exclusion row). NULL otherwise.
   const int32_t* n_users_dev;
   const int64_t* pos_map;
-  uint64_t* cand;  // [n_chunks][n_users_pad][CAP] keys (unsorted)
-  int32_t* cnt;    // [n_chunks][n_users_pad] valid keys per buffer
+  uint64_t* cand;  // [buffer rows][CAP] keys (unsorted)
+  int32_t* cnt;    // [buffer rows] valid keys per buffer
   uint64_t* diag;  // [gridDim.x * kWaves][kDgSlots] in DR_TOPK_DIAG builds
 };
 
@@ -618,18 +635,33 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
     n_users = n < n_users ? n : n_users;
     n_ublocks = (n_users + UPWG - 1) / UPWG;
   }
-  const int64_t n_units = n_ublocks * a.n_chunks;
+  const int64_t n_head = a.n_head < n_ublocks ? a.n_head : n_ublocks;
+  const int64_t n_tail = n_ublocks - n_head;
+  const int64_t n_units = n_head + n_tail * a.tail_chunks;
   for (int64_t unit = blockIdx.x; unit < n_units; unit += gridDim.x) {
     DG_T0(t_pro);
-    const int64_t chunk = unit / n_ublocks;
-    const int64_t ub = unit % n_ublocks;
-    const int64_t i_beg = chunk * a.chunk_items;
-    int64_t i_end = i_beg + a.chunk_items;
-    i_end = i_end < a.n_items ? i_end : a.n_items;
+    int64_t ub, i_beg = 0, i_end = a.n_items, brow;
+    bool chunked = false;  // a tail chunk unit: compacted down to end_keep at its end
+    if (unit < n_head) {
+      ub = unit;
+      brow = ub * UPWG;
+    } else {
+      const int64_t idx = unit - n_head;
+      const int64_t j = idx / n_tail, tb = idx % n_tail;
+      ub = n_head + tb;
+      i_beg = j * a.chunk_items;
+      i_end = i_beg + a.chunk_items < a.n_items ? i_beg + a.chunk_items : a.n_items;
+      brow = j == 0 ? ub * UPWG : a.n_users_pad + ((j - 1) * n_tail + tb) * UPWG;
+      chunked = a.tail_chunks > 1;
+    }
     const int ntiles = i_end > i_beg ? (int)((i_end - i_beg + kTileItems - 1) / kTileItems) : 0;
     const int nst = (ntiles + SR - 1) / SR;
     const int64_t upos0 = ub * UPWG + (int64_t)wave * UPW;  // first user position of the wave
-    uint64_t* cbase = a.cand + ((size_t)chunk * a.n_users_pad + upos0) * CAP;
+    const int64_t brow0 = brow + (int64_t)wave * UPW;      // its first buffer row
+    // the unit's last compaction test: a chunk of a split tail block keeps at
+    // most end_keep keys per user, so the finalize gathers a bounded count
+    const int last_lim = (chunked && a.end_keep > 0 && a.end_keep < flush_at) ? a.end_keep : flush_at;
+    uint64_t* cbase = a.cand + (size_t)brow0 * CAP;
 
     // Resident B fragments: lane holds user (ut*32+col), k = 16s + 8h .. +7.
     u32x4 bfr[NU_T][KS];  // bf16x8 (bf16 tables) or f32x4 (fp32 tables) per k-step
@@ -717,11 +749,11 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       DG_CNT(kDgNFlush);
     };
 
-    auto check_compact = [&]() {
+    auto check_compact = [&](int lim) {
 #pragma unroll
       for (int ut = 0; ut < NU_T; ++ut) {
         const uint32_t c_cnt = ucnt[ut * 32 + col];
-        uint64_t need = __ballot(c_cnt > (uint32_t)flush_at) & 0xffffffffull;
+        uint64_t need = __ballot(c_cnt > (uint32_t)lim) & 0xffffffffull;
         while (need) {
           const int c = __builtin_ctzll(need);
           need &= need - 1;
@@ -985,12 +1017,13 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         // end of a stage: resolve the staged blocks, compact full buffers
         if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) {
           if (nblk > 0) resolve(IC<DR_RESOLVE_BATCHED>{});
-          check_compact();
+          check_compact(flush_at);
         }
       } else {
         if (hit_bits != 0u) enqueue(t, acc, hit_bits, GI);
         // end of a stage: compact the buffers that passed flush_at
-        if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) check_compact();
+        if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles))
+          check_compact(flush_at);
       }
     };
     // One accumulator set: the partner wave on the same SIMD issues its MFMAs
@@ -1010,10 +1043,11 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         epilogue(t, acc, IC<1>{});
       }
     }
+    // a chunk of a split tail block ends with at most end_keep keys per user
+    if (last_lim < flush_at && ntiles > 0) check_compact(last_lim);
     wait_vmcnt<0>();
     wave_lds_sync();
-    for (int s = lane; s < UPW; s += 64)
-      a.cnt[(size_t)chunk * a.n_users_pad + upos0 + s] = (int32_t)ucnt[s];
+    for (int s = lane; s < UPW; s += 64) a.cnt[(size_t)brow0 + s] = (int32_t)ucnt[s];
     __syncthreads();  // the ring is refilled by the next unit
   }
 #ifdef DR_TOPK_DIAG
@@ -1033,11 +1067,15 @@ struct Plan {
   int users_per_wg;
   int64_t n_ublocks;
   int64_t n_users_pad;
-  int n_chunks;
-  int64_t chunk_items;
+  int64_t n_head;       // user blocks scanned whole (one unit each)
+  int tail_chunks;      // catalog chunks per tail block (1 = no split)
+  int64_t chunk_items;  // tail chunk length
+  int end_keep;         // keys a tail chunk buffer keeps at its end (0: no end compaction)
+  int64_t buf_rows;     // candidate buffers: n_users_pad + the tail's extra chunks
   int grid;
   size_t cand_bytes;
   size_t cnt_bytes;
+  int64_t head_users() const { return n_head * users_per_wg; }
 };
 
 // Launch the scan for rows of width W (bf16 units) on stream s; defined per

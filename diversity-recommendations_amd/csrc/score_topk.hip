@@ -17,6 +17,8 @@
 // Keys encode (score desc, item asc) as one 64-bit unsigned order, so the
 // result is a deterministic total order and any item partition (chunks,
 // GPUs) gives bit-identical top-k lists.
+#include <cstdlib>
+
 #include "score_scan.h"
 
 namespace {
@@ -24,35 +26,50 @@ namespace {
 using namespace dr_topk;
 
 // ------------------------------------------------------------------ per-user gather
-// One user's candidate keys of every chunk into registers (element e = lane*P
-// + i), excluded items dropped; 0 = empty.
+// Where a user's candidate buffers live (Plan / TopkArgs): every user has its
+// chunk-0 buffer at row = its position; a user of a split tail block has
+// chunks - 1 more at rows n_users_pad + (j - 1) * tail_pad + (u - head_users).
+struct BufMap {
+  int64_t n_users_pad;
+  int64_t head_users;  // positions below this have one buffer
+  int64_t tail_pad;    // users of the split tail blocks
+  int chunks;          // buffers of a tail user
+  __device__ int64_t row(int64_t u, int j) const {
+    return j == 0 ? u : n_users_pad + (int64_t)(j - 1) * tail_pad + (u - head_users);
+  }
+  __device__ int n(int64_t u) const { return u < head_users ? 1 : chunks; }
+};
+
+BufMap buf_map(const Plan& p) {
+  return BufMap{p.n_users_pad, p.head_users(), (p.n_ublocks - p.n_head) * p.users_per_wg,
+                p.tail_chunks};
+}
+
+// One user's candidate keys of every buffer into registers (element e =
+// lane*P + i), excluded items dropped; 0 = empty. The plan bounds the count
+// by 64*P.
 template <int P>
 __device__ __forceinline__ void gather_candidates(const uint64_t* __restrict__ cand,
-                                                  const int32_t* __restrict__ cnt, int n_chunks,
-                                                  int cap, int64_t u, int64_t n_users_pad,
+                                                  const int32_t* __restrict__ cnt, const BufMap m,
+                                                  int cap, int64_t u,
                                                   const int64_t* __restrict__ excl_rowptr,
                                                   const int32_t* __restrict__ excl_items,
                                                   int64_t er, uint64_t (&key)[P]) {
   const int lane = dr::lane_id();
-  int off[9];
-  off[0] = 0;
-  for (int c = 0; c < 8; ++c)
-    off[c + 1] = off[c] + (c < n_chunks ? cnt[(size_t)c * n_users_pad + u] : 0);
-  const int total = off[8];
 #pragma unroll
-  for (int i = 0; i < P; ++i) {
-    const int e = lane * P + i;
-    uint64_t v = 0ull;
-    if (e < total) {
-      int c = 0;
+  for (int i = 0; i < P; ++i) key[i] = 0ull;
+  const int nc = m.n(u);
+  int off = 0;
+  for (int c = 0; c < nc; ++c) {
+    const int64_t r = m.row(u, c);
+    const int n = cnt[r];
+    const uint64_t* src = cand + (size_t)r * cap;
 #pragma unroll
-      for (int q = 1; q < 8; ++q) c += (e >= off[q]) ? 1 : 0;
-      int base = off[0];
-#pragma unroll
-      for (int q = 1; q < 8; ++q) base = (c == q) ? off[q] : base;
-      v = cand[((size_t)c * n_users_pad + u) * cap + (e - base)];
+    for (int i = 0; i < P; ++i) {
+      const int e = lane * P + i;
+      if (e >= off && e < off + n) key[i] = src[e - off];
     }
-    key[i] = v;
+    off += n;
   }
   if (excl_rowptr) {  // er: the user's exclusion row
     const int64_t e0 = excl_rowptr[er], e1 = excl_rowptr[er + 1];
@@ -65,8 +82,8 @@ __device__ __forceinline__ void gather_candidates(const uint64_t* __restrict__ c
 }
 
 // ------------------------------------------------------------------ finalize
-// One wave per user: all chunks' candidate keys -> drop excluded items ->
-// wave-wide register bitonic sort -> k best, decoded.
+// One wave per user of [u0, n_users): all its candidate buffers -> drop
+// excluded items -> wave-wide register bitonic sort -> k best, decoded.
 //   * Guessed-threshold scans (fail_cnt != NULL): a user left with fewer than
 //     k keys may have lost items to a threshold guessed too high; it is
 //     appended to the fail list (its user row and position) for the rescan.
@@ -74,15 +91,15 @@ __device__ __forceinline__ void gather_candidates(const uint64_t* __restrict__ c
 //     caller's position pos_map[u]; the count comes from the device.
 template <int P>
 __global__ __launch_bounds__(256) void topk_finalize_kernel(
-    const uint64_t* __restrict__ cand, const int32_t* __restrict__ cnt, int n_chunks, int cap,
-    int64_t n_users, int64_t n_users_pad, int k, const int64_t* __restrict__ excl_rowptr,
+    const uint64_t* __restrict__ cand, const int32_t* __restrict__ cnt, const BufMap m, int cap,
+    int64_t u0, int64_t n_users, int k, const int64_t* __restrict__ excl_rowptr,
     const int32_t* __restrict__ excl_items, float* __restrict__ out_s,
     int32_t* __restrict__ out_i, const int64_t* __restrict__ pos_map,
     const int32_t* __restrict__ n_users_dev, const int64_t* __restrict__ user_ids,
     int32_t* __restrict__ fail_cnt, int64_t* __restrict__ fail_rows,
     int64_t* __restrict__ fail_pos) {
   const int lane = dr::lane_id();
-  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t u = u0 + (((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6);
   if (n_users_dev) {
     const int64_t n = *n_users_dev;
     n_users = n < n_users ? n : n_users;
@@ -90,7 +107,7 @@ __global__ __launch_bounds__(256) void topk_finalize_kernel(
   if (u >= n_users) return;  // wave-uniform
   const int64_t op = pos_map ? pos_map[u] : u;  // output and exclusion row
   uint64_t key[P];
-  gather_candidates<P>(cand, cnt, n_chunks, cap, u, n_users_pad, excl_rowptr, excl_items, op, key);
+  gather_candidates<P>(cand, cnt, m, cap, u, excl_rowptr, excl_items, op, key);
   dr::wave_sort_desc<P>(key);
 #pragma unroll
   for (int i = 0; i < P; ++i) {
@@ -109,24 +126,24 @@ __global__ __launch_bounds__(256) void topk_finalize_kernel(
 }
 
 // ------------------------------------------------------------------ threshold
-// One wave per user position of the sample scan: the starting threshold of the
-// main scan, strictly below the user's k-th best (non-excluded) sample score,
-// so every score >= it passes the scan's `score > thr` test. -inf when the
-// sample holds fewer than k candidates; +inf for padding positions (no user).
+// One wave per user position of [u0, u1) of the sample scan: the starting
+// threshold of the main scan, strictly below the user's k-th best
+// (non-excluded) sample score, so every score >= it passes the scan's
+// `score > thr` test. -inf when the sample holds fewer than k candidates;
+// +inf for padding positions (no user).
 template <int P>
 __global__ __launch_bounds__(256) void topk_threshold_kernel(
-    const uint64_t* __restrict__ cand, const int32_t* __restrict__ cnt, int n_chunks, int cap,
-    int64_t n_users, int64_t n_users_pad, int k, const int64_t* __restrict__ excl_rowptr,
-    const int32_t* __restrict__ excl_items, float* __restrict__ thr) {
+    const uint64_t* __restrict__ cand, const int32_t* __restrict__ cnt, const BufMap m, int cap,
+    int64_t u0, int64_t u1, int64_t n_users, int k, float* __restrict__ thr) {
   const int lane = dr::lane_id();
-  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-  if (u >= n_users_pad) return;  // wave-uniform
+  const int64_t u = u0 + (((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6);
+  if (u >= u1) return;  // wave-uniform
   if (u >= n_users) {
     if (lane == 0) thr[u] = INFINITY;
     return;
   }
   uint64_t key[P];
-  gather_candidates<P>(cand, cnt, n_chunks, cap, u, n_users_pad, excl_rowptr, excl_items, u, key);
+  gather_candidates<P>(cand, cnt, m, cap, u, nullptr, nullptr, u, key);
   dr::wave_sort_desc<P>(key);
   const int e = k - 1;
   if (lane == e / P) {
@@ -186,7 +203,14 @@ int p_for(int total) {
 
 // ------------------------------------------------------------------ planning
 // Plans take w, the row width in bf16 units (d for bf16 tables, 2d for fp32).
+// Workgroup slots = CUs (one 512-thread workgroup per CU). DIVREC_SCAN_SLOTS
+// overrides the count so that tests can reach the split-tail plans with
+// small inputs; the result is identical for any plan.
 int device_cus() {
+  if (const char* e = getenv("DIVREC_SCAN_SLOTS")) {
+    const int v = atoi(e);
+    if (v > 0) return v;
+  }
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -207,38 +231,78 @@ int cap_for(int w, int k) {
   return -1;
 }
 
-Plan make_plan(int64_t n_users, int64_t n_items, int w, int k) {
+constexpr int kMaxTailChunks = 16;
+// The finalize of a split-tail user sorts every chunk's end-compacted keys
+// (<= k + kSlack each) in one wave; at most 1024 of them keeps its sort at
+// P = 16 (a 2048-key sort costs ~6x the 512-key one of a whole-catalog user).
+constexpr int kMaxTailKeys = 1024;
+
+// Grid tail: U users make B = ceil(U / UPWG) user blocks for `slots`
+// workgroups. Whole-catalog units run in ceil(B / slots) rounds, the last one
+// with B % slots of the CUs busy (1M users at d = 128: 977 blocks, the 4th
+// round on 209 of 256 CUs, 4.6 % of the scan idle). The plan keeps
+// H = floor(B / slots) * slots "head" blocks whole and splits each of the T
+// tail blocks into c catalog chunks, c chosen to minimise
+// H / slots + ceil(T c / slots) / c (in whole-unit times); the chunks'
+// buffers are merged by the finalize. With B < slots, H = 0 and the chunks
+// fill the idle CUs instead.
+//
+// Measured (tools/variant_bench.py, 1M users, d = 128, k = 100, lists
+// identical; profiles/r02_scan/ab_split_*.json): the split gains less than the
+// idle-CU count suggests, because the chip clocks up while a last round runs on
+// fewer CUs: +0.7 % at 1.25M items (an 8-way shard), and at 10M items +1.5 %
+// together with the seeding it needs (a chunk scanned from -inf pays its own
+// survivor stream), which alone costs 1.1 % there at the 1/32 sample stride
+// and breaks even at 1/128. So a head/tail split is planned only for
+// catalogs the guess can seed (seedable); a grid smaller than the CU count
+// (H = 0) is chunked in any case, as before.
+Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   Plan p{};
   p.cap = cap_for(w, k);
   p.users_per_wg = nut_for(w) * 32 * kWaves;
   p.n_ublocks = dr::ceil_div(n_users, p.users_per_wg);
   p.n_users_pad = p.n_ublocks * p.users_per_wg;
-  const int slots = device_cus();  // one 512-thread workgroup per CU
+  const int64_t slots = device_cus();
   const int64_t stage_items = stage_items_for(w);
-  // Split the catalog into chunks only to balance the tail of the grid; each
-  // chunk must stay long enough to amortise its start, and the finalize
-  // kernel sorts at most 2048 candidates per user.
+  // each chunk stays long enough to amortise its start (B fragments, ring fill)
   const int64_t min_chunk = 65536;
-  int best_s = 1;
-  double best_eff = 0.0;
-  for (int s = 1; s <= 8; ++s) {
-    if (s > 1 && n_items / s < min_chunk) break;
-    if ((int64_t)s * p.cap > 2048) break;
-    const int64_t units = p.n_ublocks * s;
-    const int64_t rounds = dr::ceil_div(units, slots);
-    const double eff = (double)units / (double)(rounds * slots);
-    if (eff > best_eff + 0.02) {
-      best_eff = eff;
-      best_s = s;
+  int max_c_override = 0;
+  const int64_t B = p.n_ublocks;
+  const int64_t H = (B / slots) * slots;
+  if (H > 0 && !seedable) max_c_override = 1;
+  const int64_t T = B - H;
+  int best_c = 1;
+  double best = (double)H / slots + (double)dr::ceil_div(T, slots);
+  int max_c = max_c_override > 0 ? max_c_override : kMaxTailChunks;
+  if (const char* e = getenv("DIVREC_SCAN_SPLIT")) max_c = atoi(e) > 0 ? atoi(e) : 1;  // A/B knob
+  for (int c = 2; c <= max_c && T > 0; ++c) {
+    if (n_items / c < min_chunk) break;
+    if (c * (k + kSlack) > kMaxTailKeys) break;
+    const double t = (double)H / slots + (double)dr::ceil_div(T * c, slots) / c;
+    if (t < best * 0.99) {  // a smaller split unless a larger one gains > 1 %
+      best = t;
+      best_c = c;
     }
   }
-  p.n_chunks = best_s;
-  p.chunk_items = dr::ceil_div(dr::ceil_div(n_items, best_s), stage_items) * stage_items;
-  const int64_t units = p.n_ublocks * p.n_chunks;
+  p.n_head = best_c > 1 ? H : B;
+  p.tail_chunks = best_c;
+  p.chunk_items = best_c > 1
+      ? dr::ceil_div(dr::ceil_div(n_items, best_c), stage_items) * stage_items : n_items;
+  p.end_keep = best_c > 1 ? k + kSlack : 0;
+  p.buf_rows = p.n_users_pad + (int64_t)(best_c - 1) * (B - p.n_head) * p.users_per_wg;
+  const int64_t units = p.n_head + (B - p.n_head) * best_c;
   p.grid = (int)(units < slots ? units : slots);
-  p.cand_bytes = (size_t)p.n_chunks * p.n_users_pad * p.cap * sizeof(uint64_t);
-  p.cnt_bytes = ((size_t)p.n_chunks * p.n_users_pad * sizeof(int32_t) + 255) & ~(size_t)255;
+  p.cand_bytes = (size_t)p.buf_rows * p.cap * sizeof(uint64_t);
+  p.cnt_bytes = ((size_t)p.buf_rows * sizeof(int32_t) + 255) & ~(size_t)255;
   return p;
+}
+
+// Largest candidate count the finalize of a head / split-tail user gathers
+// (the sort instances start at 512 keys).
+int head_keys(const Plan& p) { return p.cap; }
+int tail_keys(const Plan& p) {
+  const int n = p.tail_chunks > 1 ? p.tail_chunks * p.end_keep : p.cap;
+  return n > 512 ? n : 512;
 }
 
 // Guessed thresholds (DR_GUESS). A scan that starts at -inf stores every
@@ -285,12 +349,26 @@ constexpr int64_t kGuessMaxItems = 1ll << DR_GUESS_MAX_LOG2;
 #define DR_GUESS_LONG_K 256
 #endif
 
-Guess guess_for(int64_t n_items, int k) {
+// A plan with a split tail is always seeded (from kGuessMinItems rows): an
+// unseeded chunk pays the survivor stream of its own catalog part from -inf,
+// ~c times the keys of one whole-catalog pass for its users.
+Guess guess_for(int64_t n_items, int k, bool split_tail) {
   Guess g;
   if (!DR_GUESS || n_items < kGuessMinItems) return g;
-  if (n_items > kGuessMaxItems && k < DR_GUESS_LONG_K) return g;
+  const char* force = getenv("DIVREC_SCAN_SEED");  // A/B knob: "0" never, "1" always
+  if (force && force[0] == '0') return g;
+  if (n_items > kGuessMaxItems && k < DR_GUESS_LONG_K && !split_tail && !(force && force[0] == '1'))
+    return g;
+  // Long catalogs sample more sparsely: the sample scan starts from -inf and
+  // is survivor-dense (~1.5x the per-row cost of the seeded scan), so about
+  // 2^16 sample rows are kept (stride 32 up to 2^22 rows, 64 from 4.2M,
+  // 128 from 8.4M). Measured with the split tail at 1M x 10M, d = 128:
+  // stride 32 / 64 / 128 / 256 = 1912 / 1879 / 1873 / 1880 ms
+  // (profiles/r02_scan/ab_stride_10m.json). Long lists keep stride 32.
   g.stride = kGuessStride;
-  g.S = n_items / kGuessStride;
+  while (k < DR_GUESS_LONG_K && g.stride < 128 && n_items / (2 * g.stride) >= 65536) g.stride *= 2;
+  if (const char* e = getenv("DIVREC_GUESS_STRIDE")) g.stride = atoi(e) > 1 ? atoi(e) : g.stride;  // A/B knob
+  g.S = n_items / g.stride;
   const double mu = (double)k * (double)g.S / (double)n_items;
   int ks = (int)ceil(mu + DR_GUESS_SIGMA * sqrt(mu) + 3.0);
   g.ks = ks < k ? ks : k;
@@ -326,12 +404,12 @@ struct Layout {
 
 Layout make_layout(int64_t n_users, int64_t n_items, int w, int k) {
   Layout L{};
-  L.main = make_plan(n_users, n_items, w, k);
-  L.g = guess_for(n_items, k);
+  L.main = make_plan(n_users, n_items, w, k, DR_GUESS && n_items >= kGuessMinItems);
+  L.g = guess_for(n_items, k, L.main.tail_chunks > 1);
   L.cand = L.main.cand_bytes;
   L.cnt = L.main.cnt_bytes;
   if (L.g.S > 0) {
-    L.sample = make_plan(n_users, L.g.S, w, L.g.ks);
+    L.sample = make_plan(n_users, L.g.S, w, L.g.ks, false);
     L.cand = L.cand > L.sample.cand_bytes ? L.cand : L.sample.cand_bytes;
     L.cnt = L.cnt > L.sample.cnt_bytes ? L.cnt : L.sample.cnt_bytes;
     L.thr = al256((size_t)L.main.n_users_pad * sizeof(float));
@@ -476,17 +554,19 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   a.k = k;
   a.excl_rowptr = excl_rowptr;
   a.excl_items = excl_items;
-  a.n_chunks = p.n_chunks;
-  a.chunk_items = p.chunk_items;
   a.n_ublocks = p.n_ublocks;
+  a.n_head = p.n_head;
+  a.tail_chunks = p.tail_chunks;
+  a.chunk_items = p.chunk_items;
+  a.end_keep = p.end_keep;
   a.init_thr = nullptr;
   a.n_users_dev = nullptr;
   a.pos_map = nullptr;
   a.cand = (uint64_t*)ws;
   a.cnt = (int32_t*)(ws + L.cand);
   a.diag = (uint64_t*)(ws + L.off_diag());  // written only in DIAG builds
-  const int fin_grid = (int)dr::ceil_div(n_users, 4);
-  const int P = p_for(p.n_chunks * p.cap);
+  const BufMap bm = buf_map(p);
+  const int64_t head_end = p.head_users() < n_users ? p.head_users() : n_users;
 
 #define DR_SCAN_OR_FAIL(PLAN, ARGS, SEEDED)                                  \
   if (!launch_scan(PLAN, ARGS, dtype, w, SEEDED, s)) {                       \
@@ -502,20 +582,31 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
       dr::set_error("dr_score_topk: internal plan error (candidate sort)"); \
       return DR_EUNSUPPORTED;                                              \
   }
-#define DR_FIN(PP, POS, NDEV, FCNT)                                                             \
-  hipLaunchKernelGGL((topk_finalize_kernel<PP>), dim3(fin_grid), dim3(256), 0, s, a.cand, a.cnt, \
-                     p.n_chunks, p.cap, n_users, p.n_users_pad, k, excl_rowptr, excl_items,     \
-                     out_scores, out_items, POS, NDEV, user_ids, FCNT, frows, fpos)
+  // finalize of users [U0, U1) (one wave each), P sized for their key count
+#define DR_FIN(PP)                                                                             \
+  hipLaunchKernelGGL((topk_finalize_kernel<PP>), dim3((unsigned)dr::ceil_div(U1 - U0, 4)),      \
+                     dim3(256), 0, s, a.cand, a.cnt, FMAP, p.cap, U0, U1, k, excl_rowptr,        \
+                     excl_items, out_scores, out_items, FPOS, FNDEV, user_ids, FCNT, frows, fpos)
+  // head users (one buffer each), then the split tail's users (their chunks)
+#define DR_FIN_ALL()                                                        \
+  {                                                                         \
+    const BufMap FMAP = bm;                                                 \
+    int64_t U0 = 0, U1 = head_end;                                          \
+    if (U1 > U0) { DR_BY_P(p_for(head_keys(p)), DR_FIN) DR_CHECK_LAUNCH(); } \
+    U0 = head_end;                                                          \
+    U1 = n_users;                                                           \
+    if (U1 > U0) { DR_BY_P(p_for(tail_keys(p)), DR_FIN) DR_CHECK_LAUNCH(); } \
+  }
 
   if (L.g.S == 0) {
     DR_SCAN_OR_FAIL(p, a, false)
     DR_CHECK_LAUNCH();
     int64_t* frows = nullptr;
     int64_t* fpos = nullptr;
-#define DR_FIN_PLAIN(PP) DR_FIN(PP, nullptr, nullptr, nullptr)
-    DR_BY_P(P, DR_FIN_PLAIN)
-#undef DR_FIN_PLAIN
-    DR_CHECK_LAUNCH();
+    const int64_t* FPOS = nullptr;
+    const int32_t* FNDEV = nullptr;
+    int32_t* FCNT = nullptr;
+    DR_FIN_ALL()
     return DR_OK;
   }
 
@@ -533,6 +624,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
                        (const uint4*)item_table, L.g.stride, L.g.S, cpr, (uint4*)samp);
     DR_CHECK_LAUNCH();
   }
+  const Plan& ps = L.sample;
   TopkArgs as = a;  // sample ids are sample rows: no exclusions, no item base
   as.I = samp;
   as.n_items = L.g.S;
@@ -540,43 +632,63 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   as.k = L.g.ks;
   as.excl_rowptr = nullptr;
   as.excl_items = nullptr;
-  as.n_chunks = L.sample.n_chunks;
-  as.chunk_items = L.sample.chunk_items;
-  DR_SCAN_OR_FAIL(L.sample, as, false)
+  as.n_head = ps.n_head;
+  as.tail_chunks = ps.tail_chunks;
+  as.chunk_items = ps.chunk_items;
+  as.end_keep = ps.end_keep;
+  DR_SCAN_OR_FAIL(ps, as, false)
   DR_CHECK_LAUNCH();
-  const int thr_grid = (int)dr::ceil_div(p.n_users_pad, 4);
-#define DR_THR(PP)                                                                              \
-  hipLaunchKernelGGL((topk_threshold_kernel<PP>), dim3(thr_grid), dim3(256), 0, s, a.cand,       \
-                     a.cnt, L.sample.n_chunks, L.sample.cap, n_users, p.n_users_pad, L.g.ks,      \
-                     nullptr, nullptr, thr)
-  DR_BY_P(p_for(L.sample.n_chunks * L.sample.cap), DR_THR)
+  {
+    const BufMap sm = buf_map(ps);
+    const int64_t sh = ps.head_users();
+#define DR_THR(PP)                                                                             \
+  hipLaunchKernelGGL((topk_threshold_kernel<PP>), dim3((unsigned)dr::ceil_div(T1 - T0, 4)),     \
+                     dim3(256), 0, s, a.cand, a.cnt, sm, ps.cap, T0, T1, n_users, L.g.ks, thr)
+    int64_t T0 = 0, T1 = sh < p.n_users_pad ? sh : p.n_users_pad;
+    if (T1 > T0) { DR_BY_P(p_for(head_keys(ps)), DR_THR) DR_CHECK_LAUNCH(); }
+    T0 = T1;
+    T1 = p.n_users_pad;
+    if (T1 > T0) { DR_BY_P(p_for(tail_keys(ps)), DR_THR) DR_CHECK_LAUNCH(); }
 #undef DR_THR
-  DR_CHECK_LAUNCH();
+  }
 
   a.init_thr = thr;
   DR_SCAN_OR_FAIL(p, a, true)
   DR_CHECK_LAUNCH();
-#define DR_FIN_VERIFY(PP) DR_FIN(PP, nullptr, nullptr, fcnt)
-  DR_BY_P(P, DR_FIN_VERIFY)
-#undef DR_FIN_VERIFY
-  DR_CHECK_LAUNCH();
+  {
+    const int64_t* FPOS = nullptr;
+    const int32_t* FNDEV = nullptr;
+    int32_t* FCNT = fcnt;  // verify: users left with fewer than k keys
+    DR_FIN_ALL()
+  }
 
-  // ---- rescan of the users whose guess was too high (usually none)
+  // ---- rescan of the users whose guess was too high (usually none): whole
+  // catalog units only, one buffer per listed user
   TopkArgs af = a;
   af.init_thr = nullptr;
   af.user_ids = frows;
   af.pos_map = fpos;
   af.n_users_dev = fcnt;
+  af.n_head = p.n_ublocks;
+  af.tail_chunks = 1;
+  af.chunk_items = n_items;
+  af.end_keep = 0;
   af.diag = nullptr;
   DR_SCAN_OR_FAIL(p, af, false)
   DR_CHECK_LAUNCH();
-#define DR_FIN_RESCAN(PP) DR_FIN(PP, fpos, fcnt, nullptr)
-  DR_BY_P(P, DR_FIN_RESCAN)
-#undef DR_FIN_RESCAN
+  {
+    const BufMap FMAP{p.n_users_pad, p.n_users_pad, 0, 1};
+    const int64_t U0 = 0, U1 = n_users;
+    const int64_t* FPOS = fpos;
+    const int32_t* FNDEV = fcnt;
+    int32_t* FCNT = nullptr;
+    DR_BY_P(p_for(p.cap), DR_FIN)
+    DR_CHECK_LAUNCH();
+  }
+#undef DR_FIN_ALL
 #undef DR_FIN
 #undef DR_BY_P
 #undef DR_SCAN_OR_FAIL
-  DR_CHECK_LAUNCH();
   return DR_OK;
 }
 

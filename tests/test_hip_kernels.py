@@ -300,6 +300,96 @@ def test_score_topk_guess_rescan_many_units_exact(d):
     assert np.array_equal(s.cpu().numpy(), ref_s)
 
 
+class _Slots:
+    """Workgroup-slot count the scan planner plans for (DIVREC_SCAN_SLOTS):
+    small counts reach the split-tail plans with small inputs."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __enter__(self):
+        import os
+        self.old = os.environ.get("DIVREC_SCAN_SLOTS")
+        os.environ["DIVREC_SCAN_SLOTS"] = str(self.n)
+
+    def __exit__(self, *exc):
+        import os
+        if self.old is None:
+            os.environ.pop("DIVREC_SCAN_SLOTS", None)
+        else:
+            os.environ["DIVREC_SCAN_SLOTS"] = self.old
+
+
+def _exact_topk_torch_excl(U, I, k, frozen, block=256):
+    """_exact_topk_torch with each user's frozen items scored -inf (integer
+    tables: exact scores, stable sort = (score desc, id asc))."""
+    Ud, Id = torch.from_numpy(U).to(DEV), torch.from_numpy(I).to(DEV)
+    outi = []
+    for b in range(0, Ud.shape[0], block):
+        S = Ud[b:b + block] @ Id.T
+        for r in range(S.shape[0]):
+            f = frozen[b + r]
+            if len(f):
+                S[r, torch.from_numpy(np.asarray(f, dtype=np.int64)).to(DEV)] = -float("inf")
+        outi.append(torch.sort(S, dim=1, descending=True, stable=True).indices[:, :k].cpu())
+    return torch.cat(outi).numpy().astype(np.int64)
+
+
+@pytest.mark.parametrize("d,slots,n_full", [(128, 4, 6), (64, 3, 6), (32, 3, 3), (32, 5, 1)])
+def test_score_topk_split_tail_exact(d, slots, n_full):
+    """Grid-tail plans: with `slots` workgroup slots, the user blocks past the
+    last full round are each split into catalog chunks (DESIGN.md §3.1 grid
+    tail), their chunk buffers end-compacted and merged by the finalize. The
+    lists (with exclusions, duplicate user ids and a partial last block) must
+    equal the exact top-k."""
+    rng = np.random.default_rng(900 + d)
+    upwg = 2048 if d <= 64 else 1024
+    nu, ni, k = n_full * upwg + 333, 300_007, 50
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    users = np.concatenate([np.arange(nu - 40), rng.integers(0, nu, 40)]).astype(np.int64)
+    frozen = [rng.choice(ni, size=int(rng.integers(0, 30)), replace=False) for _ in users]
+    for n in range(0, len(users), 97):  # exclude some of the user's best items
+        best = np.argsort(-(I @ U[users[n]]), kind="stable")[:10]
+        frozen[n] = np.union1d(frozen[n], best)
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    with _Slots(slots):
+        s, it = ops.score_topk(_bf16(U), _bf16(I), k, user_ids=torch.from_numpy(users).to(DEV),
+                               exclude=(torch.from_numpy(rowptr).to(DEV),
+                                        torch.from_numpy(cols).to(DEV)))
+    ref_i = _exact_topk_torch_excl(U[users], I, k, frozen)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_score_topk_split_tail_rescan_exact(d):
+    """A split tail whose every user fails the guessed threshold (hot sampled
+    rows): the fail list comes from the chunked finalize, and the rescan
+    (whole-catalog units) rewrites every list."""
+    rng = np.random.default_rng(188 + d)
+    ni, k = (1 << 18) + 77, 20
+    nu = 2 * (2048 if d <= 64 else 1024) + 333
+    U = _int_table(rng, nu, d, 0, 3)
+    I = _int_table(rng, ni, d)
+    I[np.arange(12) * 32] = 3.0  # see test_score_topk_guess_rescan_many_units_exact
+    with _Slots(2):
+        s, it = ops.score_topk(_bf16(U), _bf16(I), k)
+    ref_i, ref_s = _exact_topk_torch(U, I, k)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy(), ref_s)
+
+
+def test_score_topk_split_tail_fp32_exact():
+    """The fp32 scan under a split-tail plan."""
+    rng = np.random.default_rng(4242)
+    nu, ni, k = 2 * 1024 + 100, 300_007, 30
+    U, I = _int_table(rng, nu, 64), _int_table(rng, ni, 64)
+    with _Slots(2):
+        s, it = ops.score_topk(torch.from_numpy(U).to(DEV), torch.from_numpy(I).to(DEV), k)
+    ref_i, ref_s = _exact_topk_torch(U, I, k)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy(), ref_s)
+
+
 def test_score_topk_guess_float_large():
     """Guessed-threshold path on a float catalog (2^19 rows, d=128): every user
     takes the guess (few or no rescans), lists within the float tolerance."""

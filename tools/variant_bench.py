@@ -4,7 +4,9 @@
     python tools/variant_bench.py --libs product,NAME,... [--users U --items I --dim D --k K]
 
 Each entry of --libs is a library tag: "product" is divrec/_lib/libdivrec_hip.so,
-any other tag T is divrec/_lib/libdivrec_hip_T.so. Every library is loaded into
+any other tag T is divrec/_lib/libdivrec_hip_T.so. A tag may carry planner
+knobs read from the environment at each call, "product@DIVREC_SCAN_SPLIT=1"
+(several joined by "+"): the same library timed under another plan. Every library is loaded into
 this one process (separate code objects), fed the same device inputs, and timed
 with HIP events on the current stream, round-robin, `--rounds` times. The
 outputs of every build must equal the first build's bit for bit (the ranking
@@ -42,6 +44,7 @@ _ABI1 = {"dr_score_topk_workspace": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_
 
 
 def lib_for(tag):
+    tag = tag.split("@")[0]
     name = "libdivrec_hip.so" if tag == "product" else f"libdivrec_hip_{tag}.so"
     lib = ctypes.CDLL(os.path.join(LIBDIR, name))
     sigs = dict(B.SIGNATURES)
@@ -70,11 +73,16 @@ def main():
     I = (torch.randn(args.items, d, generator=g, device=dev) / d ** 0.5).to(torch.bfloat16)
     tags = args.libs.split(",")
     libs = {t: lib_for(t) for t in tags}
+    envs = {t: dict(kv.split("=", 1) for kv in t.split("@")[1].split("+")) if "@" in t else {}
+            for t in tags}
     stream = torch.cuda.current_stream(dev).cuda_stream
     outs, times = {}, {t: [] for t in tags}
 
     def run(t):
         L = libs[t]
+        for key in ("DIVREC_SCAN_SPLIT", "DIVREC_SCAN_SEED", "DIVREC_SCAN_SLOTS", "DIVREC_GUESS_STRIDE"):
+            os.environ.pop(key, None)
+        os.environ.update(envs[t])
         dt = () if t.startswith("abi1") else (B.DR_BF16,)
         ws_bytes = L.dr_score_topk_workspace(args.users, args.items, *dt, d, args.k)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
