@@ -134,6 +134,15 @@ __device__ __forceinline__ T select_reg(const T (&v)[P], int idx) {
   for (int i = 1; i < P; ++i) r = (idx == i) ? v[i] : r;
   return r;
 }
+// The same for 64-bit keys as a masked OR: at P >= 16 hipcc turns the select
+// chain above back into an indexed access of a stack copy (scratch).
+template <int P>
+__device__ __forceinline__ uint64_t select_key(const uint64_t (&v)[P], int idx) {
+  uint64_t r = 0ull;
+#pragma unroll
+  for (int i = 0; i < P; ++i) r |= v[i] & (0ull - (uint64_t)(idx == i));
+  return r;
+}
 
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
   uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);

@@ -29,6 +29,8 @@ using namespace dr_topk;
 // Where a user's candidate buffers live (Plan / TopkArgs): every user has its
 // chunk-0 buffer at row = its position; a user of a split tail block has
 // chunks - 1 more at rows n_users_pad + (j - 1) * tail_pad + (u - head_users).
+constexpr int kMaxChunks = 16;  // = kMaxTailChunks (the plan's bound)
+
 struct BufMap {
   int64_t n_users_pad;
   int64_t head_users;  // positions below this have one buffer
@@ -60,24 +62,47 @@ __device__ __forceinline__ void gather_candidates(const uint64_t* __restrict__ c
   for (int i = 0; i < P; ++i) key[i] = 0ull;
   const int nc = m.n(u);
   int off = 0;
-  for (int c = 0; c < nc; ++c) {
-    const int64_t r = m.row(u, c);
-    const int n = cnt[r];
-    const uint64_t* src = cand + (size_t)r * cap;
+  // chunk loop unrolled to its static bound so key[] stays in registers
 #pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const int e = lane * P + i;
-      if (e >= off && e < off + n) key[i] = src[e - off];
+  for (int c = 0; c < kMaxChunks; ++c) {
+    if (c < nc) {
+      const int64_t r = m.row(u, c);
+      const int n = cnt[r];
+      const uint64_t* src = cand + (size_t)r * cap;
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const int e = lane * P + i;
+        if (e >= off && e < off + n) key[i] = src[e - off];
+      }
+      off += n;
     }
-    off += n;
   }
   if (excl_rowptr) {  // er: the user's exclusion row
     const int64_t e0 = excl_rowptr[er], e1 = excl_rowptr[er + 1];
+    const int n = (int)(e1 - e0);
+    const int32_t* list = excl_items + e0;
+    if (n > 0) {
+      // lower_bound of every key's item by binary lifting: one runtime loop
+      // over the (uniform) steps around the unrolled per-key work, so key[]
+      // keeps static indices (P independent searches, each a loop of its
+      // own, left key[] in scratch at P >= 16)
+      int lo[P];
 #pragma unroll
-    for (int i = 0; i < P; ++i)
-      if (key[i] != 0ull &&
-          sorted_contains(excl_items + e0, (int)(e1 - e0), (int32_t)dr::key_item(key[i])))
-        key[i] = 0ull;
+      for (int i = 0; i < P; ++i) lo[i] = 0;
+      int step = 1;
+      while (2 * step <= n) step *= 2;
+      for (; step > 0; step >>= 1) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+          const int c = lo[i] + step;
+          if (c <= n && list[c - 1] < (int32_t)dr::key_item(key[i])) lo[i] = c;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < P; ++i)
+        if (key[i] != 0ull && lo[i] < n && list[lo[i]] == (int32_t)dr::key_item(key[i]))
+          key[i] = 0ull;
+    }
   }
 }
 
@@ -118,7 +143,7 @@ __global__ __launch_bounds__(256) void topk_finalize_kernel(
       out_i[op * k + e] = empty ? -1 : (int32_t)dr::key_item(key[i]);
     }
   }
-  if (fail_cnt && lane == (k - 1) / P && dr::select_reg<P>(key, (k - 1) % P) == 0ull) {
+  if (fail_cnt && lane == (k - 1) / P && dr::select_key<P>(key, (k - 1) % P) == 0ull) {
     const int32_t f = atomicAdd(fail_cnt, 1);
     fail_rows[f] = user_ids ? user_ids[u] : u;
     fail_pos[f] = u;
@@ -147,7 +172,7 @@ __global__ __launch_bounds__(256) void topk_threshold_kernel(
   dr::wave_sort_desc<P>(key);
   const int e = k - 1;
   if (lane == e / P) {
-    const uint64_t kk = dr::select_reg<P>(key, e % P);
+    const uint64_t kk = dr::select_key<P>(key, e % P);
     float t = -INFINITY;
     if (kk != 0ull) {
       const float s = dr::key_score(kk);
