@@ -300,9 +300,11 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   double best = (double)H / slots + (double)dr::ceil_div(T, slots);
   int max_c = max_c_override > 0 ? max_c_override : kMaxTailChunks;
   if (const char* e = getenv("DIVREC_SCAN_SPLIT")) max_c = atoi(e) > 0 ? atoi(e) : 1;  // A/B knob
+  int max_keys = kMaxTailKeys;
+  if (const char* e = getenv("DIVREC_TAIL_KEYS")) max_keys = atoi(e) > 0 ? atoi(e) : max_keys;  // A/B knob
   for (int c = 2; c <= max_c && T > 0; ++c) {
     if (n_items / c < min_chunk) break;
-    if (c * (k + kSlack) > kMaxTailKeys) break;
+    if (c * (k + kSlack) > max_keys) break;
     const double t = (double)H / slots + (double)dr::ceil_div(T * c, slots) / c;
     if (t < best * 0.99) {  // a smaller split unless a larger one gains > 1 %
       best = t;

@@ -80,7 +80,8 @@ def main():
 
     def run(t):
         L = libs[t]
-        for key in ("DIVREC_SCAN_SPLIT", "DIVREC_SCAN_SEED", "DIVREC_SCAN_SLOTS", "DIVREC_GUESS_STRIDE"):
+        for key in ("DIVREC_SCAN_SPLIT", "DIVREC_SCAN_SEED", "DIVREC_SCAN_SLOTS", "DIVREC_GUESS_STRIDE",
+                    "DIVREC_TAIL_KEYS"):
             os.environ.pop(key, None)
         os.environ.update(envs[t])
         dt = () if t.startswith("abi1") else (B.DR_BF16,)
