@@ -101,3 +101,26 @@ def test_ops_fail_loudly_without_gpu():
     t = torch.zeros(4, 64)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ops.gather_dot(t, t, torch.zeros(2, dtype=torch.int64), torch.zeros(2, dtype=torch.int64))
+
+
+def test_workspace_reflects_split_tail_plan(monkeypatch):
+    """The planner (host only) splits the grid tail: 1M users at d=128 are 977
+    user blocks for 256 workgroup slots, so 768 blocks scan the 10M catalog
+    whole and each of the 209 tail blocks is split into 6 chunks, whose extra
+    candidate buffers (5 x 209 x 1024 rows of CAP 512 keys) the workspace
+    holds; with the split off (DIVREC_SCAN_SPLIT=1) only one buffer per user
+    remains (DESIGN.md §3.1 grid tail)."""
+    lib = _backend.load_library()
+    bf16 = _backend.DR_BF16
+    monkeypatch.setenv("DIVREC_SCAN_SLOTS", "256")
+    one = (1_000_000 + 448) * 512 * 8  # padded users x CAP x 8 B
+    extra = 5 * 209 * 1024 * 512 * 8
+    split = lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100)
+    assert one + extra <= split < one + extra + 200_000_000
+    monkeypatch.setenv("DIVREC_SCAN_SPLIT", "1")
+    whole = lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100)
+    assert one <= whole < one + 100_000_000
+    # a grid of exactly one full round has no tail to split
+    monkeypatch.delenv("DIVREC_SCAN_SPLIT")
+    full = lib.dr_score_topk_workspace(256 * 1024, 10_000_000, bf16, 128, 100)
+    assert full < 256 * 1024 * 512 * 8 + 100_000_000
