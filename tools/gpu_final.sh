@@ -1,7 +1,7 @@
 #!/bin/bash
-# End-of-session GPU pass: parity suite, smoke, headline bench with its CPU
-# baseline, rocprofv3 kernel summary of the headline, every secondary line,
-# and the PMC passes of the kernels changed this round (BPR, MMR).
+# End-of-session GPU pass, part 1: parity suite, smoke, headline bench with its
+# CPU baseline, rocprofv3 kernel summary of the headline, every secondary
+# workload line. Part 2 (PMC traffic): bash tools/gpu_pmc_kernels.sh catalog mmr
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -14,4 +14,3 @@ cd $GRAFT_REPO_ROOT
 for w in score1m gather bpr mmr fp32 ml100k; do
   timeout -k 10 300 python bench.py --workload $w > gpurun_out/f_wl_$w.json 2> gpurun_out/f_wl_$w.err
 done
-bash tools/gpu_pmc_kernels.sh bpr mmr
