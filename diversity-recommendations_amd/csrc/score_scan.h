@@ -152,7 +152,17 @@ struct TileGeom {
 constexpr int nut_for(int w) {
   return w >= 512 ? 1 : (w >= 256 ? 2 : (w <= 64 ? DR_NUT_NARROW : DR_NUT));
 }
-constexpr int ngroup_for(int w) { return nut_for(w) > 4 ? 4 : nut_for(w); }
+#ifndef DR_PINGPONG
+// Two user-tile groups with one accumulator set EACH, software-pipelined: the
+// epilogue of one group runs while the other group's MFMAs execute (the wave
+// issues VALU under its own MFMAs), instead of both groups sharing one set
+// and every epilogue waiting for the MFMA chain before it. Needs NU_T <= 6
+// (two sets of NU_T/2 tiles = 96 VGPRs beside 96 of B fragments).
+#define DR_PINGPONG 0
+#endif
+constexpr int ngroup_for(int w) {
+  return (nut_for(w) > 4 || (DR_PINGPONG && w <= 64)) ? nut_for(w) / 2 : nut_for(w);
+}
 template <int V>
 struct IC {
   static constexpr int value = V;
@@ -1026,6 +1036,51 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
           check_compact(flush_at);
       }
     };
+    if constexpr (DR_PINGPONG && NGRP == 2) {
+      // Ping-pong: tile t's group-0 MFMAs are issued, then group 1's epilogue
+      // of tile t-1 runs under them; group 1's MFMAs of tile t are issued,
+      // then group 0's epilogue of tile t runs under them. The stage-end work
+      // (resolve, compaction) follows group 1's epilogue of a stage's last
+      // tile, so both groups are complete through the stage when it runs; a
+      // user still gets at most one stage of keys between two compactions.
+      f32x16 acc0[NG], acc1[NG];
+      auto stage_end = [&](int t_last, int lim) {
+        if constexpr (STAGED) {
+          if (nblk > 0) resolve(IC<DR_RESOLVE_BATCHED>{});
+        }
+        check_compact(lim);
+        (void)t_last;
+      };
+      auto epi = [&](int t, f32x16 (&acc)[NG], auto GI) {
+        DG_T0(t_h);
+        uint32_t hit_bits = any_hits(acc, GI);
+        DG_ADD(kDgHits, t_h);
+        hit_bits = __builtin_amdgcn_readfirstlane(hit_bits);
+        if (hit_bits != 0u) {
+          if constexpr (STAGED) stage_hits(t, acc, hit_bits, GI);
+          else enqueue(t, acc, hit_bits, GI);
+        }
+      };
+      for (int t = 0; t < ntiles; ++t) {
+        DG_CNT(kDgNTiles);
+        if (t % SR == 0) boundary(t / SR);
+        DG_T0(t_m);
+        mma_tile(t, acc0, IC<0>{});
+        DG_ADD(kDgMma, t_m);
+        if (t > 0) {
+          epi(t - 1, acc1, IC<1>{});
+          if (t % SR == 0) stage_end(t - 1, flush_at);
+        }
+        DG_T0(t_m2);
+        mma_tile(t, acc1, IC<1>{});
+        DG_ADD(kDgMma, t_m2);
+        epi(t, acc0, IC<0>{});
+      }
+      if (ntiles > 0) {
+        epi(ntiles - 1, acc1, IC<1>{});
+        stage_end(ntiles - 1, flush_at);
+      }
+    } else {
     // One accumulator set: the partner wave on the same SIMD issues its MFMAs
     // while this wave runs the epilogue (two waves per SIMD by design).
     f32x16 acc[NG];
@@ -1042,6 +1097,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         DG_ADD(kDgMma, t_m2);
         epilogue(t, acc, IC<1>{});
       }
+    }
     }
     // a chunk of a split tail block ends with at most end_keep keys per user
     if (last_lim < flush_at && ntiles > 0) check_compact(last_lim);
