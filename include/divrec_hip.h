@@ -103,7 +103,9 @@ int dr_gather_dot_backward(const float* user_table, int64_t n_user_rows, const f
  *     base_datasets.py:143-149). Both NULL = no exclusion.
  *   out_scores fp32 [n_users, k], out_items int32 [n_users, k] (GLOBAL ids);
  *     slots with no candidate hold item -1 and score -inf.
- *   workspace of dr_score_topk_workspace(...) bytes (query with identical args).
+ *   workspace of dr_score_topk_workspace(...) bytes (query with identical args,
+ *     with the device that runs the call current: the launch plan, and with it
+ *     the size, depends on the device's CU count).
  */
 size_t dr_score_topk_workspace(int64_t n_users, int64_t n_items, int dtype, int d, int k);
 int dr_score_topk(const void* user_table, const int64_t* user_ids, int64_t n_users,
