@@ -85,7 +85,8 @@ def parse():
                     help="after timing, recompute this many of each rank's final users "
                          "over the whole catalog on one device and require identical lists")
     ap.add_argument("--workload", default="catalog",
-                    choices=["catalog", "score1m", "gather", "bpr", "mmr", "fp32", "ml100k"])
+                    choices=["catalog", "score1m", "gather", "bpr", "mmr", "fp32", "ml100k",
+                             "excl"])
     ap.add_argument("--candidates", type=int, default=1000, help="mmr: top-C candidates per user")
     ap.add_argument("--mmr-k", type=int, default=100, help="mmr: re-ranked list length")
     ap.add_argument("--mmr-lambda", type=float, default=0.5)
@@ -564,6 +565,39 @@ def secondary(args):
 
     if args.workload == "ml100k":
         return ml100k(args, dev, g)
+
+    if args.workload == "excl":
+        # the headline shape with a 100-items/user exclusion CSR
+        # (RankingDataset's frozen items, base_datasets.py:145-151): the
+        # compaction and the finalize drop excluded keys by binary search.
+        # Timed beside the same call without exclusions, in one process.
+        U_n, I_n, d, k, n_ex = args.users, args.items, args.dim, args.k, 100
+        users, items = gen_table(U_n, d, 1, dev), gen_table(I_n, d, 2, dev)
+        ex = torch.sort(torch.randint(0, I_n, (U_n, n_ex), generator=g, device=dev,
+                                      dtype=torch.int32), dim=1).values
+        # distinct items per user: a sorted row with repeats bumped past them
+        # would need a loop; instead drop the repeats and keep the CSR ragged
+        keep = torch.ones_like(ex, dtype=torch.bool)
+        keep[:, 1:] = ex[:, 1:] != ex[:, :-1]
+        cnt = keep.sum(1).to(torch.int64)
+        rowptr = torch.zeros(U_n + 1, dtype=torch.int64, device=dev)
+        rowptr[1:] = torch.cumsum(cnt, 0)
+        cols = ex[keep].contiguous()
+        wall0, dt0 = _timed(lambda: ops.score_topk(users, items, k), args.steps, args.warmup)
+        wall, dt = _timed(lambda: ops.score_topk(users, items, k, exclude=(rowptr, cols)),
+                          args.steps, args.warmup)
+        flops = 2.0 * U_n * I_n * d
+        _line("scored pairs/sec with a 100-items/user exclusion CSR, 1M x 10M d=128 top-100 "
+              "(SURVEY.md 8d)", U_n * I_n / wall, "scored pairs/s", args, wall, "bf16",
+              {"workload": f"score_topk {U_n} users x {I_n} items d={d} k={k}, "
+                           f"{int(cols.numel())} excluded (user, item) pairs", "users": U_n,
+               "items": I_n, "dim": d, "k": k, "excluded_per_user": n_ex},
+              {"bound": "mfma", "achieved": flops / dt / 1e12, "peak": MFMA_BF16_PEAK_TFLOPS,
+               "unit": "TFLOP/s", "frac": flops / dt / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+               "traffic": None, "kernel": "dr_score_topk with exclusions"}, None,
+              no_exclusion_ms=dt0 * 1e3, exclusion_ms=dt * 1e3,
+              exclusion_overhead=dt / dt0 - 1.0)
+        return 0
 
     if args.workload == "fp32":
         # MatrixFactorization.score_topk's default (fp32-faithful) mode on the
