@@ -559,7 +559,8 @@ def secondary(args):
                "items": I_n, "dim": d, "k": k},
               {"bound": "mfma", "achieved": flops / dt / 1e12, "peak": MFMA_BF16_PEAK_TFLOPS,
                "unit": "TFLOP/s", "frac": flops / dt / 1e12 / MFMA_BF16_PEAK_TFLOPS,
-               "traffic": load_traffic(f"U{U_n}_I{I_n}_d{d}_k{k}_G1"),
+               "traffic": (pmc_traffic("score1m", f"U{U_n}_I{I_n}_d{d}_k{k}_G1", SCAN_KERNELS)
+                           or load_traffic(f"U{U_n}_I{I_n}_d{d}_k{k}_G1")),
                "kernel": "dr_score_topk (sample scan + thresholds + seeded scan + finalize)"}, cpu)
         return 0
 
@@ -617,7 +618,8 @@ def secondary(args):
                "scan_width": w, "k": k},
               {"bound": "mfma", "achieved": flops_pad / dt / 1e12, "peak": MFMA_F32_PEAK_TFLOPS,
                "unit": "TFLOP/s", "frac": flops_pad / dt / 1e12 / MFMA_F32_PEAK_TFLOPS,
-               "traffic": None, "flop_per_launch": flops_pad,
+               "traffic": pmc_traffic("fp32", f"fp32_U{U_n}_I{I_n}_d{d}_k{k}", SCAN_KERNELS),
+               "flop_per_launch": flops_pad,
                "kernel": "dr_score_topk, fp32 scan (v_mfma_f32_32x32x2_f32) + finalize; flops "
                          "counted at the padded width"},
               None, useful_tflops=2.0 * U_n * I_n * d / dt / 1e12)
@@ -794,7 +796,9 @@ def secondary(args):
         mxm = {"value": nb / mw, "unit": "triples/s", "ms": mdt * 1e3, "triples": nb,
                "layout": f"PairWiseDataset m x m (m = {m_s}, {n_su} users in order)",
                "row_runs": n_runs, "atomic_rows_per_triple": n_runs / nb,
-               "hbm_roofline": dict(_hbm(mxm_bytes, mdt), per_unit="ids + loss/hit per triple, "
+               "hbm_roofline": dict(_hbm(mxm_bytes, mdt, pmc_traffic("bpr", "bpr", "bpr_kernel",
+                                                                       group=2)),
+                                    per_unit="ids + loss/hit per triple, "
                                     "one row read + one row of atomic adds per run of equal ids")}
         gU.zero_()
         gI.zero_()

@@ -4,7 +4,8 @@
 # (FETCH_SIZE, WRITE_SIZE: separate runs, MI355X_MICROARCH.md HBM section),
 # reduced by tools/pmc_kernels.py to per-dispatch bytes. bench.py reads the
 # resulting profiles/pmc_<workload>.json into roofline.traffic.
-#   usage: bash tools/gpu_pmc_kernels.sh [workload ...]   (default: gather bpr mmr catalog)
+#   usage: bash tools/gpu_pmc_kernels.sh [workload ...]   (default: gather bpr mmr catalog;
+#   also score1m fp32)
 # Every GPU step has its own time limit; the first failure ends the script.
 set -e
 mkdir -p gpurun_out/pmck
@@ -17,6 +18,8 @@ for w in $WL; do
     bpr) args="--workload bpr --steps 1 --warmup 1"; cfg=bpr; lim=240 ;;
     mmr) args="--workload mmr --steps 1 --warmup 0"; cfg=mmr_U1000000_I10000000_d128_C1000_k100; lim=300 ;;
     catalog) args="--steps 1 --warmup 0"; cfg=U1000000_I10000000_d128_k100_G1; lim=240 ;;
+    score1m) args="--workload score1m --steps 1 --warmup 0"; cfg=U1000000_I1000000_d64_k100_G1; lim=240 ;;
+    fp32) args="--workload fp32 --steps 1 --warmup 0"; cfg=fp32_U262144_I1000000_d100_k100; lim=240 ;;
     *) echo "unknown workload $w"; exit 1 ;;
   esac
   reps=$(python3 -c "import re,sys; a=sys.argv[1]; print(int(re.search(r'--steps (\d+)',a).group(1))+int(re.search(r'--warmup (\d+)',a).group(1)))" "$args")
