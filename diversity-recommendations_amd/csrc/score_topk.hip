@@ -324,12 +324,23 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   return p;
 }
 
-// Largest candidate count the finalize of a head / split-tail user gathers
-// (the sort instances start at 512 keys).
-int head_keys(const Plan& p) { return p.cap; }
-int tail_keys(const Plan& p) {
-  const int n = p.tail_chunks > 1 ? p.tail_chunks * p.end_keep : p.cap;
-  return n > 512 ? n : 512;
+// Largest candidate count the finalize of a head / split-tail user gathers.
+// A whole-catalog buffer ends with at most flush_at keys (the scan compacts
+// every buffer above flush_at = min(k + kSlack + kFlushGap, CAP - margin) at
+// each stage end, the last included), so k = 100 sorts 256 keys, not CAP = 512
+// (the sort instances start at 256 keys).
+int flush_keys(const Plan& p, int w, int k) {
+  const int f = k + kSlack + kFlushGap;
+  const int m = p.cap - (int)stage_items_for(w);
+  return f < m ? f : m;
+}
+int head_keys(const Plan& p, int w, int k) {
+  const int n = flush_keys(p, w, k);
+  return n > 256 ? n : 256;
+}
+int tail_keys(const Plan& p, int w, int k) {
+  const int n = p.tail_chunks > 1 ? p.tail_chunks * p.end_keep : flush_keys(p, w, k);
+  return n > 256 ? n : 256;
 }
 
 // Guessed thresholds (DR_GUESS). A scan that starts at -inf stores every
@@ -602,6 +613,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   }
 #define DR_BY_P(PP_EXPR, LAUNCH)                                           \
   switch (PP_EXPR) {                                                       \
+    case 4: LAUNCH(4); break;                                              \
     case 8: LAUNCH(8); break;                                              \
     case 16: LAUNCH(16); break;                                            \
     case 32: LAUNCH(32); break;                                            \
@@ -619,10 +631,10 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   {                                                                         \
     const BufMap FMAP = bm;                                                 \
     int64_t U0 = 0, U1 = head_end;                                          \
-    if (U1 > U0) { DR_BY_P(p_for(head_keys(p)), DR_FIN) DR_CHECK_LAUNCH(); } \
+    if (U1 > U0) { DR_BY_P(p_for(head_keys(p, w, k)), DR_FIN) DR_CHECK_LAUNCH(); } \
     U0 = head_end;                                                          \
     U1 = n_users;                                                           \
-    if (U1 > U0) { DR_BY_P(p_for(tail_keys(p)), DR_FIN) DR_CHECK_LAUNCH(); } \
+    if (U1 > U0) { DR_BY_P(p_for(tail_keys(p, w, k)), DR_FIN) DR_CHECK_LAUNCH(); } \
   }
 
   if (L.g.S == 0) {
@@ -672,10 +684,10 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   hipLaunchKernelGGL((topk_threshold_kernel<PP>), dim3((unsigned)dr::ceil_div(T1 - T0, 4)),     \
                      dim3(256), 0, s, a.cand, a.cnt, sm, ps.cap, T0, T1, n_users, L.g.ks, thr)
     int64_t T0 = 0, T1 = sh < p.n_users_pad ? sh : p.n_users_pad;
-    if (T1 > T0) { DR_BY_P(p_for(head_keys(ps)), DR_THR) DR_CHECK_LAUNCH(); }
+    if (T1 > T0) { DR_BY_P(p_for(head_keys(ps, w, L.g.ks)), DR_THR) DR_CHECK_LAUNCH(); }
     T0 = T1;
     T1 = p.n_users_pad;
-    if (T1 > T0) { DR_BY_P(p_for(tail_keys(ps)), DR_THR) DR_CHECK_LAUNCH(); }
+    if (T1 > T0) { DR_BY_P(p_for(tail_keys(ps, w, L.g.ks)), DR_THR) DR_CHECK_LAUNCH(); }
 #undef DR_THR
   }
 
@@ -709,7 +721,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
     const int64_t* FPOS = fpos;
     const int32_t* FNDEV = fcnt;
     int32_t* FCNT = nullptr;
-    DR_BY_P(p_for(p.cap), DR_FIN)
+    DR_BY_P(p_for(head_keys(p, w, k)), DR_FIN)
     DR_CHECK_LAUNCH();
   }
 #undef DR_FIN_ALL
