@@ -304,8 +304,8 @@ struct CompactResult {
 // caller spilled its B fragments inside the MFMA loop (5x slower tiles).
 template <int P>
 __device__ DR_COMPACT_INLINE CompactResult compact_buffer_chunked(uint64_t* __restrict__ buf, int n_in, int k,
-                                                     const int32_t* __restrict__ ex, int exn,
-                                                     uint32_t* __restrict__ hist) {
+                                                     int slack, const int32_t* __restrict__ ex,
+                                                     int exn, uint32_t* __restrict__ hist) {
   constexpr int CH = 64 * P;
   const int lane = dr::lane_id();
   const int nch = (n_in + CH - 1) / CH;
@@ -338,7 +338,7 @@ __device__ DR_COMPACT_INLINE CompactResult compact_buffer_chunked(uint64_t* __re
   if (exn > 0) wait_vmcnt<0>();  // the zeroed slots are visible to the passes below
   uint64_t lo = 1ull;  // keep keys >= lo (key 0 = empty slot)
   CompactResult res{total, -INFINITY};
-  if (total > k + kSlack) {
+  if (total > k + slack) {
     uint64_t pfx = 0ull;
     int need = k, above = 0, inb = total;
     for (int shift = 56; shift >= 0; shift -= 8) {
@@ -389,7 +389,7 @@ __device__ DR_COMPACT_INLINE CompactResult compact_buffer_chunked(uint64_t* __re
       need -= excl;
       above += excl;
       wave_lds_sync();  // hist is re-zeroed by the next level
-      if (above + inb <= k + kSlack) break;
+      if (above + inb <= k + slack) break;
     }
     lo = pfx;
     res.kept = above + inb;
@@ -422,8 +422,8 @@ __device__ DR_COMPACT_INLINE CompactResult compact_buffer_chunked(uint64_t* __re
 // in registers spilled the d = 64 tile loop).
 template <int P>
 __device__ DR_COMPACT_INLINE CompactResult compact_buffer_resident(uint64_t* __restrict__ buf, int n_in, int k,
-                                                     const int32_t* __restrict__ ex, int exn,
-                                                     uint32_t* __restrict__ hist) {
+                                                     int slack, const int32_t* __restrict__ ex,
+                                                     int exn, uint32_t* __restrict__ hist) {
   const int lane = dr::lane_id();
   wait_vmcnt<0>();  // this wave's candidate stores have landed
   uint64_t key[P];
@@ -444,7 +444,7 @@ __device__ DR_COMPACT_INLINE CompactResult compact_buffer_resident(uint64_t* __r
   for (int i = 0; i < P; ++i) total += __popcll(__ballot(key[i] != 0ull));
   uint64_t lo = 1ull;  // keep keys >= lo (key 0 = empty slot)
   CompactResult res{total, -INFINITY};
-  if (total > k + kSlack) {
+  if (total > k + slack) {
     uint64_t pfx = 0ull;
     int need = k, above = 0, inb = total;
     for (int shift = 56; shift >= 0; shift -= 8) {
@@ -490,7 +490,7 @@ __device__ DR_COMPACT_INLINE CompactResult compact_buffer_resident(uint64_t* __r
       need -= excl;
       above += excl;
       wave_lds_sync();  // hist is re-zeroed by the next level
-      if (above + inb <= k + kSlack) break;
+      if (above + inb <= k + slack) break;
     }
     lo = pfx;
     res.kept = above + inb;
@@ -562,6 +562,8 @@ struct TopkArgs {
   int tail_chunks;
   int64_t chunk_items;  // multiple of the stage's item count
   int end_keep;         // tail chunk units compact buffers above this count at their end
+  int slack;            // keys a compaction keeps beyond k (kSlack; smaller for sample scans)
+  int gap;              // new keys a buffer takes past k + slack before it is compacted
   const float* init_thr;  // [n_users_pad] starting thresholds (SEEDED scans only)
   // Fallback rescan only: the user count lives on the device (n_users and
   // n_ublocks above are its upper bounds), and pos_map[p] is the caller's
@@ -606,7 +608,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
   // above k + kSlack keeps the thresholds close to the running k-th score.
   // Unseeded scans start at -inf: every score of the first stages is a
   // survivor until the first compaction sets a real threshold.
-  int flush_at = a.k + kSlack + kFlushGap;
+  int flush_at = a.k + a.slack + a.gap;
   flush_at = flush_at < CAP - G::MARGIN ? flush_at : CAP - G::MARGIN;
 
   const int wave = threadIdx.x >> 6;
@@ -746,9 +748,11 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       }
       CompactResult r;
       if constexpr (CAP <= 64 * P)
-        r = compact_buffer_resident<CAP / 64>(cbase + (size_t)slot * CAP, n_in, a.k, ex, exn, hist);
+        r = compact_buffer_resident<CAP / 64>(cbase + (size_t)slot * CAP, n_in, a.k, a.slack, ex,
+                                              exn, hist);
       else
-        r = compact_buffer_chunked<P>(cbase + (size_t)slot * CAP, n_in, a.k, ex, exn, hist);
+        r = compact_buffer_chunked<P>(cbase + (size_t)slot * CAP, n_in, a.k, a.slack, ex, exn,
+                                      hist);
       vm_done = vmc;
       if (lane == 0) ucnt[slot] = (uint32_t)r.kept;
       wave_lds_sync();
@@ -1127,6 +1131,7 @@ struct Plan {
   int tail_chunks;      // catalog chunks per tail block (1 = no split)
   int64_t chunk_items;  // tail chunk length
   int end_keep;         // keys a tail chunk buffer keeps at its end (0: no end compaction)
+  int slack, gap;       // compaction slack and flush gap (TopkArgs)
   int64_t buf_rows;     // candidate buffers: n_users_pad + the tail's extra chunks
   int grid;
   size_t cand_bytes;

@@ -257,6 +257,15 @@ int cap_for(int w, int k) {
 }
 
 constexpr int kMaxTailChunks = 16;
+// Compaction slack and flush gap of the sample scan (ks <= ~70 keys per user).
+#ifndef DR_SAMPLE_SLACK
+#define DR_SAMPLE_SLACK 32
+#endif
+#ifndef DR_SAMPLE_GAP
+#define DR_SAMPLE_GAP 96
+#endif
+constexpr int kSampleSlack = DR_SAMPLE_SLACK;
+constexpr int kSampleGap = DR_SAMPLE_GAP;
 // The finalize of a split-tail user sorts every chunk's end-compacted keys
 // (<= k + kSlack each) in one wave; at most 1024 of them keeps its sort at
 // P = 16 (a 2048-key sort costs ~6x the 512-key one of a whole-catalog user).
@@ -315,6 +324,8 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   p.tail_chunks = best_c;
   p.chunk_items = best_c > 1
       ? dr::ceil_div(dr::ceil_div(n_items, best_c), stage_items) * stage_items : n_items;
+  p.slack = kSlack;
+  p.gap = kFlushGap;
   p.end_keep = best_c > 1 ? k + kSlack : 0;
   p.buf_rows = p.n_users_pad + (int64_t)(best_c - 1) * (B - p.n_head) * p.users_per_wg;
   const int64_t units = p.n_head + (B - p.n_head) * best_c;
@@ -330,7 +341,7 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
 // each stage end, the last included), so k = 100 sorts 256 keys, not CAP = 512
 // (the sort instances start at 256 keys).
 int flush_keys(const Plan& p, int w, int k) {
-  const int f = k + kSlack + kFlushGap;
+  const int f = k + p.slack + p.gap;
   const int m = p.cap - (int)stage_items_for(w);
   return f < m ? f : m;
 }
@@ -448,6 +459,10 @@ Layout make_layout(int64_t n_users, int64_t n_items, int w, int k) {
   L.cnt = L.main.cnt_bytes;
   if (L.g.S > 0) {
     L.sample = make_plan(n_users, L.g.S, w, L.g.ks, false);
+    // the sample keeps only ks keys per user: compact it tighter
+    L.sample.slack = kSampleSlack;
+    L.sample.gap = kSampleGap;
+    if (L.sample.tail_chunks > 1) L.sample.end_keep = L.g.ks + kSampleSlack;
     L.cand = L.cand > L.sample.cand_bytes ? L.cand : L.sample.cand_bytes;
     L.cnt = L.cnt > L.sample.cnt_bytes ? L.cnt : L.sample.cnt_bytes;
     L.thr = al256((size_t)L.main.n_users_pad * sizeof(float));
@@ -597,6 +612,8 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   a.tail_chunks = p.tail_chunks;
   a.chunk_items = p.chunk_items;
   a.end_keep = p.end_keep;
+  a.slack = p.slack;
+  a.gap = p.gap;
   a.init_thr = nullptr;
   a.n_users_dev = nullptr;
   a.pos_map = nullptr;
@@ -675,6 +692,8 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   as.tail_chunks = ps.tail_chunks;
   as.chunk_items = ps.chunk_items;
   as.end_keep = ps.end_keep;
+  as.slack = ps.slack;
+  as.gap = ps.gap;
   DR_SCAN_OR_FAIL(ps, as, false)
   DR_CHECK_LAUNCH();
   {
