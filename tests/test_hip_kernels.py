@@ -390,6 +390,43 @@ def test_score_topk_split_tail_fp32_exact():
     assert np.array_equal(s.cpu().numpy(), ref_s)
 
 
+def test_score_topk_guess_large_exclusion_exact():
+    """Guessed thresholds over a 2^19+-row catalog (a 16K-row sample): integer
+    tables, several user blocks, exclusions of some users' best items,
+    duplicate ids: lists equal the exact top-k."""
+    rng = np.random.default_rng(4711)
+    d, ni, k = 64, (1 << 19) + 321, 50
+    nu = 2 * 2048 + 77
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    users = np.concatenate([np.arange(nu - 30), rng.integers(0, nu, 30)]).astype(np.int64)
+    frozen = [rng.choice(ni, size=int(rng.integers(0, 20)), replace=False) for _ in users]
+    for n in range(0, len(users), 257):
+        best = np.argsort(-(I @ U[users[n]]), kind="stable")[:15]
+        frozen[n] = np.union1d(frozen[n], best)
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    s, it = ops.score_topk(_bf16(U), _bf16(I), k, user_ids=torch.from_numpy(users).to(DEV),
+                           exclude=(torch.from_numpy(rowptr).to(DEV), torch.from_numpy(cols).to(DEV)))
+    ref_i = _exact_topk_torch_excl(U[users], I, k, frozen)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+
+
+def test_score_topk_guess_hot_sample_rows_exact():
+    """8 hot rows at catalog rows 0, 1024, ..., 7168 (all in the stride-32
+    sample) are every user's best items: the guessed rank in the sample is 9
+    (k = 20), so each threshold sits just below the user's best non-hot sample
+    score; lists and scores equal the exact top-k."""
+    rng = np.random.default_rng(99)
+    d, ni, k = 64, (1 << 19) + 77, 20
+    nu = 2048 + 100
+    U = _int_table(rng, nu, d, 0, 3)
+    I = _int_table(rng, ni, d)
+    I[np.arange(8) * 1024] = 3.0
+    s, it = ops.score_topk(_bf16(U), _bf16(I), k)
+    ref_i, ref_s = _exact_topk_torch(U, I, k)
+    assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy(), ref_s)
+
+
 def test_score_topk_guess_float_large():
     """Guessed-threshold path on a float catalog (2^19 rows, d=128): every user
     takes the guess (few or no rescans), lists within the float tolerance."""
