@@ -51,8 +51,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from divrec import ops  # noqa: E402
-from divrec.distributed import (exchange_partials, global_mean, grid_layout,  # noqa: E402
-                                shard_range)
+from divrec.distributed import (exchange_partials, global_mean, global_thresholds,  # noqa: E402
+                               grid_layout, shard_range, thresholded_exchange)
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32 (= the fp32 vector rate, MI355X_MICROARCH.md)
@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--item-shards", type=int, default=0,
                     help="ranks that row-shard the item table per user slice (0 = the world "
                          "size: pure item sharding)")
+    ap.add_argument("--local-thresholds", action="store_true",
+                    help="item shards keep their local top-k (no global sample thresholds)")
     ap.add_argument("--no-alt-grid", action="store_true",
                     help="skip timing the (N/2) x 2 grid beside the main layout (N >= 4)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -315,12 +317,22 @@ def time_layout(args, world: int, dev, S: int, record_recs: bool = True):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
         if e:
             e[0].record()
-        s, i = ops.score_topk(users, shard, k, item_base=lo)
+        if S > 1 and not args.local_thresholds:
+            # shards keep only items above per-user thresholds guessed from a
+            # sample of the whole catalog (divrec.distributed.global_thresholds)
+            thr = global_thresholds(users, shard, lo, hi, I_n, k, lay.group)
+            s, i = ops.score_topk(users, shard, k, item_base=lo, init_thr=thr)
+        else:
+            s, i = ops.score_topk(users, shard, k, item_base=lo)
         if e:
             e[1].record()
         if S > 1:  # partial lists of this rank's sub-slice from its row, merged
-            ps, pi = exchange_partials(s, i, lay.group)
-            s, i = ops.topk_merge(ps, pi, k)
+            if args.local_thresholds:
+                ps, pi = exchange_partials(s, i, lay.group)
+                s, i = ops.topk_merge(ps, pi, k)
+            else:  # exchange + merge + verification (exact fallback if a guess failed)
+                s, i = thresholded_exchange(users, shard, lo, hi, I_n, k, lay.group,
+                                            thr=thr, local=(s, i))
         if e:
             e[2].record()
         ild = ops.ild_embedding(i, items, args.ild_kind, check=False)

@@ -686,7 +686,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       const uint4* src = reinterpret_cast<const uint4*>(a.U + row * (2 * D) + 16 * h);
 #pragma unroll
       for (int s = 0; s < KS; ++s) bfr[ut][s] = __builtin_bit_cast(u32x4, src[2 * s]);
-      thr[ut] = SEEDED ? a.init_thr[pos] : -INFINITY;
+      thr[ut] = SEEDED ? (pos < n_users ? a.init_thr[pos] : INFINITY) : -INFINITY;
     }
     // Retire those loads where the compiler can see it (else it waits for them
     // inside the loop, draining the ring).

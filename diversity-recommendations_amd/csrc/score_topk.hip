@@ -750,6 +750,115 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   return DR_OK;
 }
 
+// ------------------------------------------------------------------ caller-seeded scan
+// dr_score_topk_seeded: the top-k, in the key order, of the items scoring
+// strictly above the caller's per-user threshold (the item-sharded multi-GPU
+// top-k passes thresholds guessed from a sample of the WHOLE catalog, so a
+// shard keeps only items that can reach the global top-k; divrec.distributed).
+// One seeded scan (split tail allowed) and one finalize; no guess, no verify.
+Plan seeded_plan(int64_t n_users, int64_t n_items, int w, int k) {
+  return make_plan(n_users, n_items, w, k, true);
+}
+
+extern "C" size_t dr_score_topk_seeded_workspace(int64_t n_users, int64_t n_items, int dtype,
+                                                 int d, int k) {
+  if (n_users <= 0 || n_items <= 0 || k <= 0) return 0;
+  const int w = width_for(dtype, d);
+  if (w < 0 || cap_for(w, k) < 0) return 0;
+  const Plan p = seeded_plan(n_users, n_items, w, k);
+  return p.cand_bytes + p.cnt_bytes + diag_bytes() + 256;
+}
+
+extern "C" int dr_score_topk_seeded(const void* user_table, const int64_t* user_ids,
+                                    int64_t n_users, const void* item_table, int64_t n_items,
+                                    int64_t item_base, int dtype, int d, int k,
+                                    const float* init_thr, const int64_t* excl_rowptr,
+                                    const int32_t* excl_items, float* out_scores,
+                                    int32_t* out_items, void* workspace, size_t workspace_bytes,
+                                    dr_stream_t stream) {
+  DR_CHECK_ARG(n_users >= 0 && n_items >= 0, "negative size");
+  DR_CHECK_ARG(k >= 1 && k <= 1024, "k must be in [1, 1024]");
+  DR_CHECK_ARG(dtype == DR_BF16 || dtype == DR_F32, "tables must be DR_BF16 or DR_F32");
+  const int w = width_for(dtype, d);
+  DR_CHECK_ARG(w > 0, dtype == DR_BF16 ? "bf16 d must be one of 32, 64, 128, 256, 512"
+                                       : "fp32 d must be one of 32, 64, 128, 256");
+  DR_CHECK_ARG(cap_for(w, k) > 0, "k too large for this d");
+  DR_CHECK_ARG(item_base >= 0 && item_base + n_items < 0x7fffffffLL,
+               "global item ids must fit int32");
+  DR_CHECK_ARG((excl_rowptr == nullptr) == (excl_items == nullptr),
+               "excl_rowptr and excl_items must both be set or both be NULL");
+  if (n_users == 0) return DR_OK;
+  DR_CHECK_ARG(user_table && out_scores && out_items && init_thr, "null pointer");
+  if (n_items == 0) {
+    dr::set_error("dr_score_topk_seeded: empty catalog");
+    return DR_EINVAL;
+  }
+  DR_CHECK_ARG(item_table, "null item_table");
+  hipStream_t s = (hipStream_t)stream;
+  const Plan p = seeded_plan(n_users, n_items, w, k);
+  char* ws = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  const size_t need = p.cand_bytes + p.cnt_bytes + diag_bytes();
+  if (!workspace || (size_t)(ws - (char*)workspace) + need > workspace_bytes) {
+    dr::set_error("dr_score_topk_seeded: workspace too small (need " +
+                  std::to_string(need + 256) + " bytes)");
+    return DR_EWORKSPACE;
+  }
+  TopkArgs a{};
+  a.U = (const char*)user_table;
+  a.user_ids = user_ids;
+  a.n_users = n_users;
+  a.n_users_pad = p.n_users_pad;
+  a.I = (const char*)item_table;
+  a.n_items = n_items;
+  a.item_base = item_base;
+  a.k = k;
+  a.excl_rowptr = excl_rowptr;
+  a.excl_items = excl_items;
+  a.n_ublocks = p.n_ublocks;
+  a.n_head = p.n_head;
+  a.tail_chunks = p.tail_chunks;
+  a.chunk_items = p.chunk_items;
+  a.end_keep = p.end_keep;
+  a.slack = p.slack;
+  a.gap = p.gap;
+  a.init_thr = init_thr;
+  a.cand = (uint64_t*)ws;
+  a.cnt = (int32_t*)(ws + p.cand_bytes);
+  a.diag = (uint64_t*)(ws + p.cand_bytes + p.cnt_bytes);
+  if (!launch_scan(p, a, dtype, w, true, s)) {
+    dr::set_error("dr_score_topk_seeded: internal plan error (no scan instance)");
+    return DR_EUNSUPPORTED;
+  }
+  DR_CHECK_LAUNCH();
+  const BufMap bm = buf_map(p);
+  const int64_t head_end = p.head_users() < n_users ? p.head_users() : n_users;
+  int64_t U0 = 0, U1 = head_end;
+  for (int part = 0; part < 2; ++part) {
+    if (U1 > U0) {
+      const int P = p_for(part == 0 ? head_keys(p, w, k) : tail_keys(p, w, k));
+      const dim3 grid((unsigned)dr::ceil_div(U1 - U0, 4));
+#define DR_FIN_SEEDED(PP)                                                                       \
+  hipLaunchKernelGGL((topk_finalize_kernel<PP>), grid, dim3(256), 0, s, a.cand, a.cnt, bm, p.cap, \
+                     U0, U1, k, excl_rowptr, excl_items, out_scores, out_items, nullptr, nullptr,  \
+                     user_ids, nullptr, nullptr, nullptr)
+      switch (P) {
+        case 4: DR_FIN_SEEDED(4); break;
+        case 8: DR_FIN_SEEDED(8); break;
+        case 16: DR_FIN_SEEDED(16); break;
+        case 32: DR_FIN_SEEDED(32); break;
+        default:
+          dr::set_error("dr_score_topk_seeded: internal plan error (candidate sort)");
+          return DR_EUNSUPPORTED;
+      }
+#undef DR_FIN_SEEDED
+      DR_CHECK_LAUNCH();
+    }
+    U0 = head_end;
+    U1 = n_users;
+  }
+  return DR_OK;
+}
+
 extern "C" int dr_topk_merge(const float* in_scores, const int32_t* in_items, int parts,
                              int64_t n_users, int k_in, int k_out, float* out_scores,
                              int32_t* out_items, dr_stream_t stream) {

@@ -45,6 +45,11 @@ SIGNATURES = {
         _i32,
         [_p, _p, _i64, _p, _i64, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _sz, _p],
     ),
+    "dr_score_topk_seeded_workspace": (_sz, [_i64, _i64, _i32, _i32, _i32]),
+    "dr_score_topk_seeded": (
+        _i32,
+        [_p, _p, _i64, _p, _i64, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _sz, _p],
+    ),
     "dr_topk_merge": (_i32, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p]),
     "dr_ild_dense": (_i32, [_p, _i32, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "dr_ild_labels": (_i32, [_p, _i32, _i64, _i32, _p, _i64, _p, _p, _p]),

@@ -31,6 +31,7 @@ collective is ``global_mean``, one all_reduce of (sum, count).
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass
 from typing import Any, Callable, Optional, Tuple
 
@@ -126,6 +127,138 @@ def global_mean(values: torch.Tensor, group=None) -> torch.Tensor:
     return (src[0] / src[1]).to(torch.float32).to(values.device)
 
 
+# --------------------------------------------------------------------------- global thresholds
+# Each shard of a pure item sharding would otherwise keep its LOCAL top-k: a
+# survivor stream of ~k (1 + ln(I_shard / k)) keys per user on every one of
+# the S shards, where only ~k / S of each shard's items can reach the global
+# top-k. So the ranks first agree on a per-user threshold guessed from a
+# strided sample of the WHOLE catalog (the same rule as dr_score_topk's own
+# guess: stride by catalog length, rank ks = mean + 6 sigma + 3 of the user's
+# top-k inside the sample), and each shard keeps only items above it
+# (dr_score_topk_seeded). The guess is verified after the merge: a user left
+# with fewer than k items is recomputed with plain per-shard top-k lists, so
+# the result is the exact global top-k in every case.
+GUESS_SIGMA = 6.0
+
+
+def sample_stride(n_items: int, k: int) -> int:
+    """The sample stride of dr_score_topk's guess (csrc/score_topk.hip guess_for)."""
+    st = 32
+    while k < 256 and st < 128 and n_items // (2 * st) >= 65536:
+        st *= 2
+    return st
+
+
+def guess_rank(k: int, frac: float) -> int:
+    mu = k * frac
+    return min(k, int(math.ceil(mu + GUESS_SIGMA * math.sqrt(mu) + 3.0)))
+
+
+def threshold_below(kth: torch.Tensor) -> torch.Tensor:
+    """A threshold strictly below each score (topk_threshold_kernel's rule);
+    -inf where there is no finite score."""
+    below = kth - torch.clamp(kth.abs() * 2.0 ** -20, min=2.0 ** -100)
+    return torch.where(below < kth, below, torch.full_like(kth, -math.inf))
+
+
+def _all_gather_rows(x: torch.Tensor, sizes, group) -> torch.Tensor:
+    """Concatenate every rank's x (rank p holds sizes[p] rows) in rank order."""
+    world = len(sizes)
+    m = max(max(sizes), 1)
+    staged = x.is_cuda and dist.get_backend(group) == "gloo"
+    src = x.cpu() if staged else x
+    pad = torch.zeros((m,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+    pad[: src.shape[0]] = src
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad, group=group)
+    out = torch.cat([o[: sizes[p]] for p, o in enumerate(outs)])
+    return out.to(x.device) if staged else out
+
+
+def global_thresholds(user_table: torch.Tensor, item_shard: torch.Tensor, lo: int, hi: int,
+                      n_items: int, k: int, group, user_ids: Optional[torch.Tensor] = None,
+                      local_topk: Optional[Callable[..., Partial]] = None) -> torch.Tensor:
+    """Per-user thresholds for all n users from a sample of the whole catalog:
+    every rank contributes its shard's rows at global positions j * stride,
+    the samples are all_gathered, each rank ranks ITS merge slice of users
+    against them and the thresholds are all_gathered back. fp32 [n]."""
+    if local_topk is None:
+        from divrec import ops
+
+        local_topk = ops.score_topk
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    st = sample_stride(n_items, k)
+    j0, j1 = -(-lo // st), -(-hi // st)
+    rows = item_shard[j0 * st - lo: hi - lo: st]
+    sizes = []
+    for p in range(world):
+        plo, phi = shard_range(n_items, world, p)
+        sizes.append(max(0, -(-phi // st) - -(-plo // st)))
+    sample = _all_gather_rows(rows.contiguous(), sizes, group)
+    n = user_table.size(0) if user_ids is None else user_ids.numel()
+    u_lo, u_hi = shard_range(n, world, rank)
+    ks = guess_rank(k, sample.size(0) / n_items) if sample.size(0) else 0
+    thr = torch.full((u_hi - u_lo,), -math.inf, dtype=torch.float32, device=user_table.device)
+    if ks and u_hi > u_lo and sample.size(0) >= ks:
+        ids = (user_ids[u_lo:u_hi] if user_ids is not None
+               else torch.arange(u_lo, u_hi, device=user_table.device))
+        s, _ = local_topk(user_table, sample, ks, user_ids=ids, item_base=0)
+        thr = threshold_below(s[:, ks - 1].contiguous())
+    usizes = [shard_range(n, world, p)[1] - shard_range(n, world, p)[0] for p in range(world)]
+    return _all_gather_rows(thr, usizes, group)
+
+
+def thresholded_exchange(user_table: torch.Tensor, item_shard: torch.Tensor, lo: int, hi: int,
+                         n_items: int, k: int, group, user_ids: Optional[torch.Tensor] = None,
+                         local_topk: Optional[Callable[..., Partial]] = None,
+                         merge: Optional[Callable[[torch.Tensor, torch.Tensor, int], Partial]] = None,
+                         thr: Optional[torch.Tensor] = None,
+                         local: Optional[Partial] = None) -> Partial:
+    """Top-k of this rank's merge slice over the sharded catalog with global
+    thresholds (computed here unless given): thresholded shard lists ->
+    all_to_all -> merge -> verification, with an exact fallback for users the
+    guess failed (a user with fewer than min(k, n_items) merged items)."""
+    if local_topk is None or merge is None:
+        from divrec import ops
+
+        local_topk = local_topk or ops.score_topk
+        merge = merge or ops.topk_merge
+    if thr is None:
+        thr = global_thresholds(user_table, item_shard, lo, hi, n_items, k, group, user_ids,
+                                local_topk)
+    if local is None:  # this shard's thresholded lists (the bench passes its timed call's)
+        local = local_topk(user_table, item_shard, k, user_ids=user_ids, item_base=lo,
+                           init_thr=thr)
+    s, i = local
+    ps, pi = exchange_partials(s, i, group)
+    out_s, out_i = merge(ps, pi, k)
+    # verification: the guess failed for a user left with fewer than k items
+    need = min(k, n_items)
+    bad = ((out_i[:, :need] < 0).any(dim=1)).nonzero().flatten()
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    n = user_table.size(0) if user_ids is None else user_ids.numel()
+    u_lo, _ = shard_range(n, world, rank)
+    mine = torch.tensor([bad.numel()], dtype=torch.int64, device=out_i.device)
+    counts = _all_gather_rows(mine, [1] * world, group)
+    cnt = [int(c) for c in counts.cpu()]
+    if sum(cnt) == 0:
+        return out_s, out_i
+    # exact fallback: plain per-shard top-k of every failed user, all_gathered
+    pos = _all_gather_rows((bad + u_lo).to(torch.int64), cnt, group)
+    fids = user_ids[pos] if user_ids is not None else pos
+    fs, fi = local_topk(user_table, item_shard, k, user_ids=fids, item_base=lo,
+                        init_thr=torch.full((len(pos),), -math.inf, dtype=torch.float32,
+                                            device=out_s.device))
+    gs = _all_gather_rows(fs.contiguous(), [len(pos)] * world, group).view(world, len(pos), k)
+    gi = _all_gather_rows(fi.contiguous(), [len(pos)] * world, group).view(world, len(pos), k)
+    off = sum(cnt[:rank])
+    if bad.numel():
+        ms, mi = merge(gs[:, off:off + bad.numel()].contiguous(),
+                       gi[:, off:off + bad.numel()].contiguous(), k)
+        out_s[bad], out_i[bad] = ms, mi
+    return out_s, out_i
+
+
 def sharded_score_topk(
     user_table: torch.Tensor,
     item_shard: torch.Tensor,
@@ -135,8 +268,13 @@ def sharded_score_topk(
     group=None,
     local_topk: Optional[Callable[..., Partial]] = None,
     merge: Optional[Callable[[torch.Tensor, torch.Tensor, int], Partial]] = None,
+    n_items: Optional[int] = None,
+    global_thr: bool = False,
 ) -> Tuple[Partial, Tuple[int, int]]:
     """Top-k of this rank's user slice over the whole (sharded) catalog.
+    ``global_thr`` (needs ``n_items``, the whole catalog's row count): shards
+    keep only items above thresholds guessed from a sample of the whole
+    catalog (thresholded_exchange); same result.
 
     Returns ((scores, items) for users [u_lo, u_hi), (u_lo, u_hi)); positions
     refer to ``user_ids`` if given, else to user rows 0..n-1. ``local_topk`` /
@@ -151,6 +289,11 @@ def sharded_score_topk(
     world = 1 if group is _SOLO else dist.get_world_size(group)
     rank = 0 if group is _SOLO else dist.get_rank(group)
     n = user_table.size(0) if user_ids is None else user_ids.numel()
+    if global_thr and world > 1:
+        out = thresholded_exchange(user_table, item_shard, item_base,
+                                   item_base + item_shard.size(0), n_items, k, group, user_ids,
+                                   local_topk, merge)
+        return out, shard_range(n, world, rank)
     s, i = local_topk(user_table, item_shard, k, user_ids=user_ids, item_base=item_base)
     if world == 1:
         return (s, i), (0, n)

@@ -130,9 +130,15 @@ def score_topk(
     n_users: Optional[int] = None,
     item_base: int = 0,
     exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+    init_thr: Optional[torch.Tensor] = None,
 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Top-k items per user over the catalog slice ``item_table`` (global ids
     ``item_base + row``); order = score desc, item id asc.
+
+    ``init_thr`` (fp32 [n], optional): only items scoring strictly above the
+    user's threshold are ranked (dr_score_topk_seeded); slots past the last
+    such item hold item -1 / score -inf. Used by the item-sharded multi-GPU
+    top-k with thresholds from a sample of the whole catalog.
 
     The tables' dtype picks the arithmetic: bf16 tables run the bf16 MFMA scan
     (exact products, fp32 sums: the fast mode), fp32 tables the fp32 MFMA scan
@@ -166,7 +172,8 @@ def score_topk(
         n = user_table.size(0) if n_users is None else int(n_users)
         _need(0 <= n <= user_table.size(0), "n_users out of range")
     n_items = item_table.size(0)
-    _need(k <= n_items or exclude is not None or n_items == 0, "k must be <= number of items")
+    _need(k <= n_items or exclude is not None or init_thr is not None or n_items == 0,
+          "k must be <= number of items")
     rowptr = cols = None
     if exclude is not None:
         rowptr, cols = exclude
@@ -182,6 +189,20 @@ def score_topk(
         return scores, items
     L = B.lib()
     dt = B.dtype_code(user_table.dtype)
+    if init_thr is not None:
+        B.require_device(init_thr)
+        _need(init_thr.dtype == torch.float32 and init_thr.numel() == n,
+              "init_thr must be fp32 [n_users]")
+        init_thr = init_thr.contiguous()
+        ws_bytes = L.dr_score_topk_seeded_workspace(n, n_items, dt, w, k)
+        ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=dev)
+        rc = L.dr_score_topk_seeded(
+            user_table.data_ptr(), B.ptr(user_ids), n, item_table.data_ptr(), n_items,
+            int(item_base), dt, w, int(k), init_thr.data_ptr(), B.ptr(rowptr), B.ptr(cols),
+            scores.data_ptr(), items.data_ptr(), ws.data_ptr(), ws.numel(), B.stream(dev),
+        )
+        B.check(rc, "dr_score_topk_seeded")
+        return scores, items
     ws_bytes = L.dr_score_topk_workspace(n, n_items, dt, w, k)
     ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=dev)
     rc = L.dr_score_topk(

@@ -114,6 +114,22 @@ int dr_score_topk(const void* user_table, const int64_t* user_ids, int64_t n_use
                   float* out_scores, int32_t* out_items, void* workspace,
                   size_t workspace_bytes, dr_stream_t stream);
 
+/* dr_score_topk with caller-given per-user thresholds: the top-k (same order)
+ * of the items whose score is STRICTLY above init_thr[u]; slots past the last
+ * such item hold item -1 and score -inf. init_thr fp32 [n_users] (-inf = plain
+ * top-k). The item-sharded multi-GPU top-k passes thresholds guessed from a
+ * sample of the whole catalog, so each shard returns only items that can
+ * reach the global top-k (divrec.distributed.sharded_score_topk; replaces the
+ * per-shard share of divrec/train/utils.py:53-77). Other arguments as
+ * dr_score_topk; workspace of dr_score_topk_seeded_workspace(...) bytes.
+ */
+size_t dr_score_topk_seeded_workspace(int64_t n_users, int64_t n_items, int dtype, int d, int k);
+int dr_score_topk_seeded(const void* user_table, const int64_t* user_ids, int64_t n_users,
+                         const void* item_table, int64_t n_items, int64_t item_base, int dtype,
+                         int d, int k, const float* init_thr, const int64_t* excl_rowptr,
+                         const int32_t* excl_items, float* out_scores, int32_t* out_items,
+                         void* workspace, size_t workspace_bytes, dr_stream_t stream);
+
 /* Merge `parts` per-user top-k lists (each sorted by the order above) into one:
  *   in_scores/in_items [parts, n_users, k_in] -> out [n_users, k_out], k_out <= parts*k_in
  *   (k_out <= 1024 when parts*k_in > 2048; entries with item -1 are empty).

@@ -226,3 +226,78 @@ def test_user_sharded_ild_mean():
     want = float(oracle.reduce_values(vals, "mean"))
     for _, m in got:
         assert m == pytest.approx(want, rel=1e-6)
+
+
+def _local_topk_thr(user_table, item_shard, k, user_ids=None, item_base=0, init_thr=None):
+    """CPU checker of dr_score_topk_seeded: integer tables (exact scores); the
+    top-k of the items scoring strictly above init_thr, padded with -1/-inf."""
+    U = user_table.numpy() if user_ids is None else user_table.numpy()[user_ids.numpy()]
+    S = U.astype(np.float64) @ item_shard.numpy().astype(np.float64).T
+    if init_thr is not None:
+        S = np.where(S > init_thr.numpy()[:, None].astype(np.float64), S, -np.inf)
+    order = np.argsort(-S, axis=1, kind="stable")[:, :k]
+    s = np.take_along_axis(S, order, axis=1)
+    i = np.where(np.isfinite(s), order + item_base, -1)
+    if s.shape[1] < k:  # shard shorter than k
+        pad = k - s.shape[1]
+        s = np.pad(s, ((0, 0), (0, pad)), constant_values=-np.inf)
+        i = np.pad(i, ((0, 0), (0, pad)), constant_values=-1)
+    return torch.from_numpy(s.astype(np.float32)), torch.from_numpy(i.astype(np.int32))
+
+
+def _merge_pad(ps, pi, k):
+    s, i = ps.numpy().astype(np.float64), pi.numpy().astype(np.int64)
+    parts, n, kin = s.shape
+    s = s.transpose(1, 0, 2).reshape(n, parts * kin)
+    i = i.transpose(1, 0, 2).reshape(n, parts * kin)
+    key_s = np.where(i >= 0, s, -np.inf)
+    key_i = np.where(i >= 0, i, np.iinfo(np.int64).max)
+    order = np.lexsort((key_i, -key_s), axis=1)[:, :k]
+    so, io = np.take_along_axis(key_s, order, 1), np.take_along_axis(i, order, 1)
+    io = np.where(np.isfinite(so), io, -1)
+    return torch.from_numpy(so.astype(np.float32)), torch.from_numpy(io.astype(np.int32))
+
+
+def _thr_worker(rank, world, port, U, I, k, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard_range(I.shape[0], world, rank)
+        (s, i), (ulo, uhi) = sharded_score_topk(
+            torch.from_numpy(U), torch.from_numpy(I[lo:hi]), lo, k, local_topk=_local_topk_thr,
+            merge=_merge_pad, n_items=I.shape[0], global_thr=True)
+        q.put((rank, ulo, uhi, s.numpy(), i.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k,hot", [(2, 25, False), (3, 25, False), (4, 40, True)])
+def test_sharded_topk_global_thresholds(world, k, hot):
+    """Shards keep only items above per-user thresholds guessed from a sample
+    of the whole catalog (every 32nd global row, all_gathered): the merged
+    lists equal the single-process top-k. hot=True makes every sampled row
+    every user's best item, so the guess fails for all users (32 hot items <
+    k = 40 above the threshold) and the exact fallback recomputes them."""
+    rng = np.random.default_rng(world * 7 + k)
+    lo_v = 0 if hot else -3
+    U = rng.integers(lo_v, 4, size=(45, 16)).astype(np.float32)
+    I = rng.integers(-3, 4, size=(1001, 16)).astype(np.float32)
+    if hot:
+        I[::32] = 3.0
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, return_scores=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_thr_worker, args=(r, world, port, U, I, k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seen = 0
+    for rank, ulo, uhi, s, i in sorted(got):
+        assert np.array_equal(i, ref_i[ulo:uhi])
+        assert np.array_equal(s, ref_s[ulo:uhi].astype(np.float32))
+        seen += uhi - ulo
+    assert seen == U.shape[0]

@@ -427,6 +427,38 @@ def test_score_topk_guess_hot_sample_rows_exact():
     assert np.array_equal(s.cpu().numpy(), ref_s)
 
 
+@pytest.mark.parametrize("d,ni,slots", [(64, 5000, None), (128, 300_007, 2), (32, 300_007, None)])
+def test_score_topk_seeded_thresholds_exact(d, ni, slots):
+    """dr_score_topk_seeded: the top-k of the items scoring strictly above a
+    caller threshold per user (-inf: plain top-k; +inf: an empty list; ties at
+    the threshold excluded), lists padded with -1 / -inf; a split-tail plan
+    too (slots = 2). Integer tables: exact against a masked stable sort."""
+    rng = np.random.default_rng(d + ni)
+    nu, k = 2 * (2048 if d <= 64 else 1024) + 55, 30
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    Ud, Id = torch.from_numpy(U).to(DEV), torch.from_numpy(I).to(DEV)
+    S = Ud @ Id.T
+    top = torch.topk(S, 41, dim=1).values
+    thr = top[:, 40].clone()  # ~40 items above most thresholds
+    thr[::7] = -float("inf")
+    thr[3::11] = float("inf")
+    thr[5::13] = top[5::13, 10]  # ~10 above: padded lists
+    ctx = _Slots(slots) if slots else None
+    if ctx:
+        ctx.__enter__()
+    try:
+        s, it = ops.score_topk(_bf16(U), _bf16(I), k, init_thr=thr.contiguous())
+    finally:
+        if ctx:
+            ctx.__exit__(None, None, None)
+    M = torch.where(S > thr[:, None], S, torch.full_like(S, -float("inf")))
+    v, o = torch.sort(M, dim=1, descending=True, stable=True)
+    v, o = v[:, :k], o[:, :k]
+    ref_i = torch.where(torch.isfinite(v), o, torch.full_like(o, -1))
+    assert torch.equal(it.to(torch.int64).cpu(), ref_i.cpu())
+    assert torch.equal(s.cpu(), v.cpu())
+
+
 def test_score_topk_guess_float_large():
     """Guessed-threshold path on a float catalog (2^19 rows, d=128): every user
     takes the guess (few or no rescans), lists within the float tolerance."""

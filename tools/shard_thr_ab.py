@@ -1,0 +1,72 @@
+"""One rank's share of the item-sharded top-k on ONE GPU: a 1/S shard of the
+1M x 10M headline catalog scanned with its local top-k (dr_score_topk) and
+with per-user thresholds guessed from a sample of the whole catalog
+(dr_score_topk_seeded, divrec.distributed's global thresholds), plus the
+threshold step's own cost at the merge-slice size it has under S ranks.
+
+    python tools/shard_thr_ab.py [--shards 8] [--users 1000000] [--items 10000000]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "diversity-recommendations_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from bench import gen_table  # noqa: E402
+from divrec import ops  # noqa: E402
+from divrec.distributed import guess_rank, sample_stride, shard_range, threshold_below  # noqa: E402
+
+
+def timed(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        out = fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps, out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shards", type=int, default=8)
+    ap.add_argument("--users", type=int, default=1_000_000)
+    ap.add_argument("--items", type=int, default=10_000_000)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--k", type=int, default=100)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    users = gen_table(a.users, a.dim, 1, dev)
+    items = gen_table(a.items, a.dim, 2, dev)
+    lo, hi = shard_range(a.items, a.shards, 0)
+    shard = items[lo:hi]
+    st = sample_stride(a.items, a.k)
+    sample = items[::st].contiguous()
+    ks = guess_rank(a.k, sample.size(0) / a.items)
+    u_lo, u_hi = shard_range(a.users, a.shards, 0)
+    ids = torch.arange(u_lo, u_hi, device=dev)
+    t_thr, (s, _) = timed(lambda: ops.score_topk(users, sample, ks, user_ids=ids))
+    # thresholds of all users (every rank computes its slice; here all at once)
+    s_all, _ = ops.score_topk(users, sample, ks)
+    thr = threshold_below(s_all[:, ks - 1].contiguous())
+    t_local, (ls, li) = timed(lambda: ops.score_topk(users, shard, a.k, item_base=lo))
+    t_seed, (gs, gi) = timed(lambda: ops.score_topk(users, shard, a.k, item_base=lo, init_thr=thr))
+    # every global top-k item of this shard is in the thresholded list
+    kept = (gi >= 0).sum(1).float()
+    print(json.dumps({
+        "shards": a.shards, "users": a.users, "items": a.items, "shard_items": hi - lo,
+        "sample_stride": st, "ks": ks, "local_topk_ms": t_local, "thresholded_ms": t_seed,
+        "threshold_step_ms_per_rank": t_thr, "mean_items_kept_per_user": float(kept.mean()),
+        "gain": t_local / (t_seed + t_thr) - 1.0}), flush=True)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
