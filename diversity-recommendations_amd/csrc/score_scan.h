@@ -734,7 +734,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
     };
 
     // -------------------------------------------------------------- cold paths
-    auto compact = [&](int ut, int c, int n_in) {
+    auto compact = [&](int ut, int c, int n_in, int slack) {
       DG_T0(t_f);
       const int slot = ut * 32 + c;
       const int64_t upos = upos0 + slot;
@@ -748,10 +748,10 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       }
       CompactResult r;
       if constexpr (CAP <= 64 * P)
-        r = compact_buffer_resident<CAP / 64>(cbase + (size_t)slot * CAP, n_in, a.k, a.slack, ex,
+        r = compact_buffer_resident<CAP / 64>(cbase + (size_t)slot * CAP, n_in, a.k, slack, ex,
                                               exn, hist);
       else
-        r = compact_buffer_chunked<P>(cbase + (size_t)slot * CAP, n_in, a.k, a.slack, ex, exn,
+        r = compact_buffer_chunked<P>(cbase + (size_t)slot * CAP, n_in, a.k, slack, ex, exn,
                                       hist);
       vm_done = vmc;
       if (lane == 0) ucnt[slot] = (uint32_t)r.kept;
@@ -763,7 +763,8 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
       DG_CNT(kDgNFlush);
     };
 
-    auto check_compact = [&](int lim) {
+    // buffers above lim are compacted down to k + slack keys
+    auto check_compact = [&](int lim, int slack) {
 #pragma unroll
       for (int ut = 0; ut < NU_T; ++ut) {
         const uint32_t c_cnt = ucnt[ut * 32 + col];
@@ -771,7 +772,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         while (need) {
           const int c = __builtin_ctzll(need);
           need &= need - 1;
-          compact(ut, c, __builtin_amdgcn_readlane((int)c_cnt, c));
+          compact(ut, c, __builtin_amdgcn_readlane((int)c_cnt, c), slack);
         }
       }
     };
@@ -1031,13 +1032,13 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         // end of a stage: resolve the staged blocks, compact full buffers
         if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) {
           if (nblk > 0) resolve(IC<DR_RESOLVE_BATCHED>{});
-          check_compact(flush_at);
+          check_compact(flush_at, a.slack);
         }
       } else {
         if (hit_bits != 0u) enqueue(t, acc, hit_bits, GI);
         // end of a stage: compact the buffers that passed flush_at
         if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles))
-          check_compact(flush_at);
+          check_compact(flush_at, a.slack);
       }
     };
     if constexpr (DR_PINGPONG && NGRP == 2) {
@@ -1052,7 +1053,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
         if constexpr (STAGED) {
           if (nblk > 0) resolve(IC<DR_RESOLVE_BATCHED>{});
         }
-        check_compact(lim);
+        check_compact(lim, a.slack);
         (void)t_last;
       };
       auto epi = [&](int t, f32x16 (&acc)[NG], auto GI) {
@@ -1104,7 +1105,7 @@ __global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
     }
     }
     // a chunk of a split tail block ends with at most end_keep keys per user
-    if (last_lim < flush_at && ntiles > 0) check_compact(last_lim);
+    if (last_lim < flush_at && ntiles > 0) check_compact(last_lim, last_lim - a.k);
     wait_vmcnt<0>();
     wave_lds_sync();
     for (int s = lane; s < UPW; s += 64) a.cnt[(size_t)brow0 + s] = (int32_t)ucnt[s];

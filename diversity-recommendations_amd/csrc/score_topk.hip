@@ -17,6 +17,7 @@
 // Keys encode (score desc, item asc) as one 64-bit unsigned order, so the
 // result is a deterministic total order and any item partition (chunks,
 // GPUs) gives bit-identical top-k lists.
+#include <algorithm>
 #include <cstdlib>
 
 #include "score_scan.h"
@@ -309,11 +310,14 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   double best = (double)H / slots + (double)dr::ceil_div(T, slots);
   int max_c = max_c_override > 0 ? max_c_override : kMaxTailChunks;
   if (const char* e = getenv("DIVREC_SCAN_SPLIT")) max_c = atoi(e) > 0 ? atoi(e) : 1;  // A/B knob
-  int max_keys = kMaxTailKeys;
+  // a head user's finalize already sorts 2048 keys when its flush bound
+  // passes 1024 (k >= ~800): the tail may then gather as many
+  const int head_flush = std::min(k + kSlack + kFlushGap, p.cap - (int)stage_items);
+  int max_keys = head_flush > kMaxTailKeys ? 2048 : kMaxTailKeys;
   if (const char* e = getenv("DIVREC_TAIL_KEYS")) max_keys = atoi(e) > 0 ? atoi(e) : max_keys;  // A/B knob
   for (int c = 2; c <= max_c && T > 0; ++c) {
     if (n_items / c < min_chunk) break;
-    if (c * (k + kSlack) > max_keys) break;
+    if (c * k > max_keys) break;  // each chunk keeps at least k keys
     const double t = (double)H / slots + (double)dr::ceil_div(T * c, slots) / c;
     if (t < best * 0.99) {  // a smaller split unless a larger one gains > 1 %
       best = t;
@@ -326,7 +330,9 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
       ? dr::ceil_div(dr::ceil_div(n_items, best_c), stage_items) * stage_items : n_items;
   p.slack = kSlack;
   p.gap = kFlushGap;
-  p.end_keep = best_c > 1 ? k + kSlack : 0;
+  // a tail chunk ends with at most end_keep >= k keys, so c of them fit the
+  // finalize's max_keys
+  p.end_keep = best_c > 1 ? std::min(k + kSlack, max_keys / best_c) : 0;
   p.buf_rows = p.n_users_pad + (int64_t)(best_c - 1) * (B - p.n_head) * p.users_per_wg;
   const int64_t units = p.n_head + (B - p.n_head) * best_c;
   p.grid = (int)(units < slots ? units : slots);
@@ -462,7 +468,6 @@ Layout make_layout(int64_t n_users, int64_t n_items, int w, int k) {
     // the sample keeps only ks keys per user: compact it tighter
     L.sample.slack = kSampleSlack;
     L.sample.gap = kSampleGap;
-    if (L.sample.tail_chunks > 1) L.sample.end_keep = L.g.ks + kSampleSlack;
     L.cand = L.cand > L.sample.cand_bytes ? L.cand : L.sample.cand_bytes;
     L.cnt = L.cnt > L.sample.cnt_bytes ? L.cnt : L.sample.cnt_bytes;
     L.thr = al256((size_t)L.main.n_users_pad * sizeof(float));
