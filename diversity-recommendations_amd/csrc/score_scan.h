@@ -108,7 +108,10 @@ enum {
 #define DR_COMPACT_INLINE __noinline__
 #endif
 
-constexpr int kWaves = 8;  // two waves per SIMD: 256-register budget each
+#ifndef DR_WAVES
+#define DR_WAVES 8  // 8: two waves per SIMD (256 registers each); 4: one per SIMD (512)
+#endif
+constexpr int kWaves = DR_WAVES;
 constexpr int kThreads = kWaves * 64;
 constexpr int kTileItems = 32;
 #ifndef DR_SLACK
@@ -576,7 +579,7 @@ struct TopkArgs {
 };
 
 template <int W, int CAP, bool SEEDED, bool F32>
-__global__ __launch_bounds__(kThreads, 2) void score_scan_kernel(TopkArgs a) {
+__global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkArgs a) {
   constexpr int D = W;  // geometry is by row bytes: an fp32 row of d is a bf16 row of 2d
   using G = TileGeom<D>;
   constexpr int NU_T = nut_for(D);
