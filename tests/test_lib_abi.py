@@ -124,3 +124,21 @@ def test_workspace_reflects_split_tail_plan(monkeypatch):
     monkeypatch.delenv("DIVREC_SCAN_SPLIT")
     full = lib.dr_score_topk_workspace(256 * 1024, 10_000_000, bf16, 128, 100)
     assert full < 256 * 1024 * 512 * 8 + 100_000_000
+
+
+def test_seeded_topk_argument_errors_and_workspace():
+    """dr_score_topk_seeded (caller thresholds) checks its arguments before any
+    HIP call, and its workspace holds one seeded plan (no sample regions)."""
+    lib = _backend.load_library()
+    bf16 = _backend.DR_BF16
+    rc = lib.dr_score_topk_seeded(None, None, 10, None, 10, 0, bf16, 64, 0, None, None, None,
+                                  None, None, None, 0, None)
+    assert rc == -1 and b"k must be" in lib.dr_last_error()
+    rc = lib.dr_score_topk_seeded(None, None, 10, None, 10, 0, bf16, 64, 5, None, None, None,
+                                  None, None, None, 0, None)
+    assert rc == -1 and b"null pointer" in lib.dr_last_error()
+    assert lib.dr_score_topk_seeded(None, None, 0, None, 10, 0, bf16, 64, 5, None, None, None,
+                                    None, None, None, 0, None) == 0  # no users: no-op
+    ws = lib.dr_score_topk_seeded_workspace(1_000_000, 1_250_000, bf16, 128, 100)
+    assert ws >= (1_000_000 + 448) * 512 * 8
+    assert lib.dr_score_topk_seeded_workspace(10, 10, bf16, 48, 10) == 0
