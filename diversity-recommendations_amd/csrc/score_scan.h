@@ -82,6 +82,9 @@ enum {
 #ifndef DR_PRIO
 #define DR_PRIO 0  // static s_setprio 1 for waves 4-7 (measured: no gain)
 #endif
+#ifndef DR_DYNPRIO
+#define DR_DYNPRIO 0  // s_setprio 1 around each tile's MFMA issue (A/B knob)
+#endif
 #ifndef DR_APIPE
 #define DR_APIPE 1  // A fragments read two k-steps ahead
 #endif
@@ -1096,12 +1099,24 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
       DG_CNT(kDgNTiles);
       if (t % SR == 0) boundary(t / SR);
       DG_T0(t_m);
+#if DR_DYNPRIO
+      __builtin_amdgcn_s_setprio(1);  // MFMA issue wins the SIMD over the partner's epilogue
+#endif
       mma_tile(t, acc, IC<0>{});
+#if DR_DYNPRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
       DG_ADD(kDgMma, t_m);
       epilogue(t, acc, IC<0>{});
       if constexpr (NGRP > 1) {
         DG_T0(t_m2);
+#if DR_DYNPRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
         mma_tile(t, acc, IC<1>{});
+#if DR_DYNPRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         DG_ADD(kDgMma, t_m2);
         epilogue(t, acc, IC<1>{});
       }
