@@ -26,6 +26,9 @@
 
 namespace {
 
+#ifndef DR_MMR_ALLWAVES
+#define DR_MMR_ALLWAVES 0  // fast rounds on every wave instead of wave 0 + a barrier (A/B knob)
+#endif
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
 constexpr int kTiles = 4;                          // candidate tiles of 32 per wave
@@ -351,7 +354,14 @@ __global__ __launch_bounds__(kThreads) void mmr_batch_kernel(
     // the batch-end barrier). Lane a < 32 holds probe a. The argmax is a 32-bit
     // max of ord(value) (fused DPP); an exact tie of values falls back to the
     // lowest candidate position, so the pick is the (value desc, position asc) max.
+#if DR_MMR_ALLWAVES
+    // every wave runs the (identical) rounds: t and the picked mask stay in
+    // registers, so no post-round barrier or LDS broadcast is needed
+    uint32_t picked = 0;
+    {
+#else
     if (w == 0) {
+#endif
       const int pa = lane < kProbes ? s_pcand[lane] : -1;
       const int pitem = lane < kProbes ? s_pitem[lane] : -1;
       const float lsa = lambda * (lane < kProbes ? s_pscore[lane] : 0.f);
@@ -361,14 +371,16 @@ __global__ __launch_bounds__(kThreads) void mmr_batch_kernel(
       const uint32_t blo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bound);
       const bool first = t == 0;  // round 0 ranks without the max term: one pick, then a new batch
       bool alive = pa >= 0;
+#if !DR_MMR_ALLWAVES
       uint32_t picked = 0;
+#endif
       while (t < k_out) {
         const float val = first ? lsa : fmaf(-mu, pna, lsa);
         const uint32_t ov = alive ? dr::f32_to_ord(val) : 0u;  // live ords are > 0
         const uint32_t m = wmax_u32<32>(ov);
         if (m == 0u) {  // no live probe
           if ((bhi | blo) != 0u) break;
-          if (lane == 0) s_out[t] = -1;  // no live candidate left
+          if (w == 0 && lane == 0) s_out[t] = -1;  // no live candidate left
           ++t;
           continue;
         }
@@ -381,23 +393,30 @@ __global__ __launch_bounds__(kThreads) void mmr_batch_kernel(
         const uint32_t npos = ~(uint32_t)__builtin_amdgcn_readlane(pa, pk);
         if (m < bhi || (m == bhi && npos <= blo)) break;  // a non-probe may be better
         const float g = s_gt[gbase + pk];  // issued ahead of the bookkeeping
-        if (lane == pk) s_out[t] = pitem;
+        if (w == 0 && lane == pk) s_out[t] = pitem;
         picked |= 1u << pk;
         alive = alive && lane != pk;
         ++t;
         if (first) break;
         pna = fmaxf(pna, g);
       }
+#if !DR_MMR_ALLWAVES
       if (lane == 0) {
         s_round[0] = t;
         s_round[1] = (int)picked;
       }
+#endif
     }
     MG_ADD(kMgRounds, t_rounds);
     MG_T0(t_sync2);
+#if DR_MMR_ALLWAVES
+    t = __builtin_amdgcn_readfirstlane(t);
+    picked = (uint32_t)__builtin_amdgcn_readfirstlane((int)picked);
+#else
     lds_barrier();
     t = s_round[0];
     const uint32_t picked = (uint32_t)s_round[1];
+#endif
     MG_ADD(kMgSync2, t_sync2);
     MG_T0(t_fold);
 
