@@ -188,12 +188,11 @@ def global_thresholds(user_table: torch.Tensor, item_shard: torch.Tensor, lo: in
         local_topk = ops.score_topk
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     st = sample_stride(n_items, k)
-    j0, j1 = -(-lo // st), -(-hi // st)
+    j0 = -(-lo // st)  # first global sample position j * st inside [lo, hi)
     rows = item_shard[j0 * st - lo: hi - lo: st]
-    sizes = []
-    for p in range(world):
-        plo, phi = shard_range(n_items, world, p)
-        sizes.append(max(0, -(-phi // st) - -(-plo // st)))
+    # the shards may be any contiguous split: exchange the sample sizes first
+    mine = torch.tensor([rows.size(0)], dtype=torch.int64, device=item_shard.device)
+    sizes = [int(c) for c in _all_gather_rows(mine, [1] * world, group).cpu()]
     sample = _all_gather_rows(rows.contiguous(), sizes, group)
     n = user_table.size(0) if user_ids is None else user_ids.numel()
     u_lo, u_hi = shard_range(n, world, rank)
