@@ -189,3 +189,23 @@ def test_pmc_summaries_feed_bench_traffic(tmp_path):
     assert bench.pmc_traffic("bpr", "bpr", "bpr_kernel", per_step=2) == sum(hb) / 2
     assert bench.pmc_traffic("bpr", "other-config", "bpr_kernel") is None
     assert bench.pmc_traffic("bpr", "bpr", "bpr_kernel", group=2) is None
+
+
+def test_global_threshold_helpers():
+    """The host side of the item-sharded global thresholds mirrors the scan's
+    own guess (csrc/score_topk.hip guess_for / topk_threshold_kernel): stride
+    32 / 64 / 128 by catalog length (32 for long lists), rank = mean + 6 sigma
+    + 3, thresholds strictly below the k-th sample score and -inf without one."""
+    from divrec.distributed import guess_rank, sample_stride, threshold_below
+
+    assert sample_stride(1_000_000, 100) == 32
+    assert sample_stride(5_000_000, 100) == 64
+    assert sample_stride(10_000_000, 100) == 128
+    assert sample_stride(10_000_000, 1000) == 32
+    assert guess_rank(100, 1 / 32) == 17  # the config-2 guess (ks = 17)
+    assert guess_rank(100, 78125 / 10_000_000) == 10
+    assert guess_rank(5, 0.9) == 5  # never above k
+    s = torch.tensor([1.0, -2.5, 0.0, float("-inf"), float("nan"), 3e-39])
+    t = threshold_below(s)
+    assert bool((t[:3] < s[:3]).all()) and bool((t[5:] < s[5:]).all())
+    assert torch.isinf(t[3]) and t[3] < 0 and torch.isinf(t[4]) and t[4] < 0
