@@ -295,6 +295,38 @@ def pmc_traffic(workload: str, config: str, kernel: str, group: int = 0, per_ste
 
 
 SCAN_KERNELS = "score_scan_kernel|sample_rows_kernel|topk_threshold_kernel|topk_finalize_kernel"
+N_SIMDS = 256 * 4  # MI355X: 256 CUs x 4 SIMDs
+
+
+def pmc_mfma(workload: str, config: str, kernel: str = "score_scan_kernel"):
+    """MFMA utilisation of the scan from a committed rocprofv3 counter pass
+    (tools/gpu_pmc_mfma.sh -> tools/pmc_mfma.py -> profiles/pmc_mfma_<workload>.json):
+    SQ_VALU_MFMA_BUSY_CYCLES (cycles, = 32 per v_mfma_f32_32x32x16_bf16 on its
+    SIMD; MI355X_MICROARCH.md, per-instruction constants) over the SIMD-cycles
+    of the dispatches, GRBM_GUI_ACTIVE / 8 x 1024 SIMDs (GRBM sums the 8 XCDs).
+    Read only when the config matches; None otherwise."""
+    path = os.path.join(ROOT, "profiles", f"pmc_mfma_{workload}.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if rec.get("config") != config:
+        return None
+    k = rec.get("kernels", {}).get(kernel)
+    if not k:
+        return None
+    return {"mfma_busy_frac": k["mfma_busy_frac"], "effective_clock_ghz": k.get("clock_ghz"),
+            "mfma_busy_cycles": k["mfma_busy_cycles"], "simd_cycles": k["simd_cycles"],
+            "source": f"profiles/pmc_mfma_{workload}.json ({k.get('counters', 'SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE')})"}
+
+
+def provenance() -> dict:
+    """The build id (source hash) of the loaded libdivrec_hip.so; divrec._backend
+    has already refused a library built from other sources than the tree's."""
+    from divrec import _backend
+
+    return {"build_id": _backend.build_id()}
 
 
 def time_layout(args, world: int, dev, S: int, record_recs: bool = True):
@@ -438,9 +470,11 @@ def main():
             "traffic": traffic,
             "kernel": "dr_score_topk = score_scan_kernel (MFMA scan + fused threshold top-k) + topk_finalize_kernel; timed together",
             "flop_per_launch": flops,
+            "mfma_counters": pmc_mfma("catalog", cfg_key),
         },
         "cpu_baseline": None,
     }
+    result.update(provenance())
     if args.check_users > 0:
         result["check"] = check_lists(args, r["lay"], r["users"], r["items"], r["recs"], u_lo,
                                       U_n, k, world)
@@ -528,6 +562,7 @@ def _line(metric, value, unit, args, step_s, dtype, config, roofline, cpu, **ext
            "data": "synthetic (seeded)", "config": config, "roofline": roofline,
            "cpu_baseline": cpu}
     rec.update(extra)
+    rec.update(provenance())
     print(json.dumps(rec), flush=True)
 
 
@@ -573,6 +608,7 @@ def secondary(args):
                "unit": "TFLOP/s", "frac": flops / dt / 1e12 / MFMA_BF16_PEAK_TFLOPS,
                "traffic": (pmc_traffic("score1m", f"U{U_n}_I{I_n}_d{d}_k{k}_G1", SCAN_KERNELS)
                            or load_traffic(f"U{U_n}_I{I_n}_d{d}_k{k}_G1")),
+               "mfma_counters": pmc_mfma("score1m", f"U{U_n}_I{I_n}_d{d}_k{k}_G1"),
                "kernel": "dr_score_topk (sample scan + thresholds + seeded scan + finalize)"}, cpu)
         return 0
 
@@ -954,6 +990,7 @@ def ml100k(args, dev, g):
            "roofline": None, "cpu_baseline": cpu, "metric_values": vals,
            "note": "host-side datasets and metric plumbing dominate at this size; the reference "
                    "config runs on the CPU, this build has no CPU compute path (DESIGN.md §1)"}
+    rec.update(provenance())
     print(json.dumps(rec), flush=True)
     return 0
 
@@ -1056,13 +1093,14 @@ def mmr_pipeline(args):
                         "kernel": f"dr_score_topk k={C} (the step's dominant kernel)"},
            "mmr_roofline": dict(_hbm(per_user * n_r, mmr_s,
                                      pmc_traffic("mmr", f"mmr_U{U_n}_I{I_n}_d{d}_C{C}_k{kout}",
-                                                 "mmr_probe_kernel") if world == 1 else None),
+                                                 "mmr_batch_kernel") if world == 1 else None),
                                 kernel="dr_mmr_rerank",
                                 per_unit=f"{per_user} B/user"),
            "cpu_baseline": cpu}
     if rank == 0:
         with_measured(rec["roofline"], dev, "mfma_bf16_tflops")
         with_measured(rec["mmr_roofline"], dev, "hbm_copy_gbs")
+        rec.update(provenance())
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

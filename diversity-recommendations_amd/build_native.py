@@ -16,6 +16,10 @@ import sys
 from pathlib import Path
 
 PKG_ROOT = Path(__file__).resolve().parent
+if str(PKG_ROOT) not in sys.path:
+    sys.path.insert(0, str(PKG_ROOT))
+from divrec._buildid import source_hash  # noqa: E402  (no torch import)
+
 CSRC = PKG_ROOT / "csrc"
 INCLUDE = PKG_ROOT.parent / "include"
 OBJ_DIR = PKG_ROOT / "build" / "obj"
@@ -40,14 +44,19 @@ def _headers_mtime() -> float:
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
-def _compile(src: Path, verbose: bool, obj_dir: Path = OBJ_DIR, extra=()) -> Path:
+def _compile(src: Path, verbose: bool, obj_dir: Path = OBJ_DIR, extra=(), build_id: str = "") -> Path:
     obj = obj_dir / (src.stem + ".o")
     stamp = obj_dir / "flags.txt"
     same_flags = stamp.exists() and stamp.read_text() == " ".join(extra)
+    id_flags = ()
+    if src.name == "capi.hip":  # the translation unit that carries the build id
+        id_flags = (f'-DDR_BUILD_ID="{build_id}"',)
+        id_stamp = obj_dir / "build_id.txt"
+        same_flags = same_flags and id_stamp.exists() and id_stamp.read_text() == build_id
     if same_flags and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime,
                                                                   _headers_mtime()):
         return obj
-    cmd = [HIPCC, *CFLAGS, *extra, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *extra, *id_flags, "-c", str(src), "-o", str(obj)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -72,9 +81,11 @@ def build(jobs: int = 4, verbose: bool = False, diag: bool = False, variant: str
     obj_dir.mkdir(parents=True, exist_ok=True)
     LIB_DIR.mkdir(parents=True, exist_ok=True)
     srcs = sorted(CSRC.glob("*.hip"))
+    build_id = source_hash()
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, verbose, obj_dir, extra), srcs))
+        objs = list(ex.map(lambda s: _compile(s, verbose, obj_dir, extra, build_id), srcs))
     (obj_dir / "flags.txt").write_text(" ".join(extra))
+    (obj_dir / "build_id.txt").write_text(build_id)
     newest = max(o.stat().st_mtime for o in objs)
     if lib_path.exists() and lib_path.stat().st_mtime >= newest:
         return lib_path

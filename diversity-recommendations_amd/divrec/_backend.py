@@ -13,6 +13,8 @@ from typing import Optional
 
 import torch
 
+from divrec._buildid import source_hash
+
 LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libdivrec_hip.so"
 
 DR_F32, DR_BF16, DR_I32, DR_I64, DR_F64 = 0, 1, 2, 3, 4
@@ -36,6 +38,7 @@ _sz = ctypes.c_size_t
 # name -> (restype, argtypes); mirrors include/divrec_hip.h one to one.
 SIGNATURES = {
     "dr_version": (_i32, []),
+    "dr_build_id": (ctypes.c_char_p, []),
     "dr_last_error": (ctypes.c_char_p, []),
     "dr_gather_dot": (_i32, [_p, _i64, _p, _i64, _i32, _i64, _p, _p, _i64, _p, _p, _p]),
     "dr_gather_dot_backward": (_i32, [_p, _i64, _p, _i64, _i64, _p, _p, _i64, _p, _p, _p, _p,
@@ -91,8 +94,18 @@ def load_library() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    built, want = lib.dr_build_id().decode(), source_hash()
+    if want and built != want and os.environ.get("DIVREC_ALLOW_STALE_LIB") != "1":
+        raise RuntimeError(
+            f"{path} is stale: built from sources {built}, the tree's sources hash to {want}. "
+            "Run `python diversity-recommendations_amd/build_native.py`.")
     _LIB = lib
     return lib
+
+
+def build_id() -> str:
+    """Source hash the loaded library was compiled from (dr_build_id)."""
+    return lib().dr_build_id().decode()
 
 
 def lib() -> ctypes.CDLL:

@@ -39,6 +39,30 @@ def test_version_and_error_string():
     assert isinstance(lib.dr_last_error(), bytes)
 
 
+def test_build_id_is_the_source_hash():
+    """The loaded library carries the hash of the sources it was compiled from
+    (dr_build_id), equal to the in-tree sources' hash: the GPU records
+    (tests, smoke, bench lines) name exactly which kernels ran."""
+    from divrec import _buildid
+
+    bid = _backend.build_id()
+    assert re.fullmatch(r"[0-9a-f]{16}", bid)
+    assert bid == _buildid.source_hash()
+
+
+def test_stale_library_is_refused(tmp_path, monkeypatch):
+    """A library built from other sources than the tree's is refused at load."""
+    import shutil
+
+    stale = tmp_path / "libdivrec_hip.so"
+    shutil.copy(_backend.lib_path(), stale)
+    monkeypatch.setattr(_backend, "_LIB", None)
+    monkeypatch.setenv("DIVREC_HIP_LIB", str(stale))
+    monkeypatch.setattr(_backend, "source_hash", lambda: "0" * 16)
+    with pytest.raises(RuntimeError, match="stale"):
+        _backend.load_library()
+
+
 def test_argument_errors_without_gpu():
     lib = _backend.load_library()
     # k out of range -> DR_EINVAL with a message; nothing touches the device
