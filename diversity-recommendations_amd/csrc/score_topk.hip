@@ -557,6 +557,27 @@ extern "C" size_t dr_score_topk_workspace(int64_t n_users, int64_t n_items, int 
   return make_layout(n_users, n_items, w, k).total() + 256;
 }
 
+// The launch plan dr_score_topk would use for these arguments on the current
+// device (planner knobs included), for tests that must prove which plan they
+// ran. out[0..11] = users per workgroup, user blocks, head blocks, tail chunks,
+// chunk items, grid, candidate capacity, sample stride (0 = no guess), sample
+// rows, sample rank ks, main-scan finalize keys of a head user / a tail user.
+extern "C" int dr_score_topk_plan(int64_t n_users, int64_t n_items, int dtype, int d, int k,
+                                  int64_t* out, int n_out) {
+  DR_CHECK_ARG(n_users > 0 && n_items > 0, "sizes must be positive");
+  DR_CHECK_ARG(k >= 1 && k <= 1024, "k must be in [1, 1024]");
+  const int w = width_for(dtype, d);
+  DR_CHECK_ARG(w > 0 && cap_for(w, k) > 0, "unsupported dtype / d / k");
+  DR_CHECK_ARG(out && n_out >= 12, "out must hold 12 values");
+  const Layout L = make_layout(n_users, n_items, w, k);
+  const Plan& p = L.main;
+  const int64_t v[12] = {p.users_per_wg, p.n_ublocks, p.n_head, p.tail_chunks, p.chunk_items,
+                         p.grid, p.cap, L.g.stride, L.g.S, L.g.ks, head_keys(p, w, k),
+                         tail_keys(p, w, k)};
+  for (int i = 0; i < 12; ++i) out[i] = v[i];
+  return DR_OK;
+}
+
 #ifdef DR_TOPK_DIAG
 // Diag builds only: byte offset (from the 256-B aligned workspace base) of the
 // [grid*8][16] u64 counter block of the main scan, and its grid size.

@@ -139,6 +139,10 @@ def global_mean(values: torch.Tensor, group=None) -> torch.Tensor:
 # with fewer than k items is recomputed with plain per-shard top-k lists, so
 # the result is the exact global top-k in every case.
 GUESS_SIGMA = 6.0
+# Users of the last thresholded_exchange call, summed over the ranks of its
+# group, whose guess failed and who were recomputed by the exact fallback
+# (observability for tests and the bench; not used by the path itself).
+LAST_FALLBACK_USERS = 0
 
 
 def sample_stride(n_items: int, k: int) -> int:
@@ -240,6 +244,8 @@ def thresholded_exchange(user_table: torch.Tensor, item_shard: torch.Tensor, lo:
     mine = torch.tensor([bad.numel()], dtype=torch.int64, device=out_i.device)
     counts = _all_gather_rows(mine, [1] * world, group)
     cnt = [int(c) for c in counts.cpu()]
+    global LAST_FALLBACK_USERS
+    LAST_FALLBACK_USERS = sum(cnt)
     if sum(cnt) == 0:
         return out_s, out_i
     # exact fallback: plain per-shard top-k of every failed user, all_gathered
@@ -285,6 +291,12 @@ def sharded_score_topk(
 
         local_topk = local_topk or ops.score_topk
         merge = merge or ops.topk_merge
+    if global_thr and (n_items is None or n_items < item_base + item_shard.size(0)):
+        # checked before any collective: a failure on some ranks only, inside
+        # the sequence of collectives, would leave the others waiting
+        raise ValueError(f"global_thr needs n_items (the whole catalog's row count) >= "
+                         f"item_base + shard rows = {item_base + item_shard.size(0)}, "
+                         f"got {n_items}")
     world = 1 if group is _SOLO else dist.get_world_size(group)
     rank = 0 if group is _SOLO else dist.get_rank(group)
     n = user_table.size(0) if user_ids is None else user_ids.numel()

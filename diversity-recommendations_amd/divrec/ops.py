@@ -214,6 +214,24 @@ def score_topk(
     return scores, items
 
 
+PLAN_FIELDS = ("users_per_wg", "user_blocks", "head_blocks", "tail_chunks", "chunk_items", "grid",
+               "cap", "sample_stride", "sample_rows", "sample_rank", "head_keys", "tail_keys")
+
+
+def score_topk_plan(n_users: int, n_items: int, dtype: torch.dtype, d: int, k: int) -> dict:
+    """The launch plan dr_score_topk uses for this call shape on the current
+    device (no device work): user blocks, head/tail split, guess stride, ...
+    (PLAN_FIELDS). Tests use it to prove which plan they exercised."""
+    import ctypes
+
+    w = score_width(dtype, d)
+    out = (ctypes.c_int64 * 12)()
+    rc = B.lib().dr_score_topk_plan(int(n_users), int(n_items), B.dtype_code(dtype), w, int(k),
+                                    ctypes.addressof(out), 12)
+    B.check(rc, "dr_score_topk_plan")
+    return dict(zip(PLAN_FIELDS, (int(x) for x in out)))
+
+
 def topk_merge(
     scores: torch.Tensor, items: torch.Tensor, k_out: Optional[int] = None
 ) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -118,6 +118,17 @@ int dr_score_topk(const void* user_table, const int64_t* user_ids, int64_t n_use
                   float* out_scores, int32_t* out_items, void* workspace,
                   size_t workspace_bytes, dr_stream_t stream);
 
+/* The launch plan dr_score_topk uses for these arguments on the current device
+ * (host-only query, no device work; planner knobs DIVREC_SCAN_SLOTS /
+ * DIVREC_SCAN_SPLIT / DIVREC_TAIL_KEYS / DIVREC_SCAN_SEED / DIVREC_GUESS_STRIDE
+ * included), so tests can show which plan they exercised. out[0..11] = users per
+ * workgroup, user blocks, head blocks (scanned whole), catalog chunks per tail
+ * block (1 = no split), tail chunk length, grid, candidate capacity, sample
+ * stride of the guessed threshold (0 = plain scan), sample rows, sample rank ks,
+ * finalize keys of a head user, finalize keys of a tail user. n_out >= 12. */
+int dr_score_topk_plan(int64_t n_users, int64_t n_items, int dtype, int d, int k, int64_t* out,
+                       int n_out);
+
 /* dr_score_topk with caller-given per-user thresholds: the top-k (same order)
  * of the items whose score is STRICTLY above init_thr[u]; slots past the last
  * such item hold item -1 and score -inf. init_thr fp32 [n_users] (-inf = plain

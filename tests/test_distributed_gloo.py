@@ -301,3 +301,69 @@ def test_sharded_topk_global_thresholds(world, k, hot):
         assert np.array_equal(s, ref_s[ulo:uhi].astype(np.float32))
         seen += uhi - ulo
     assert seen == U.shape[0]
+
+
+def _thr8_worker(rank, world, port, U, I, k, bounds, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from divrec import distributed
+        from divrec.distributed import grid_layout
+
+        lay = grid_layout(world)  # pure item sharding (S = world): bench.py's default at 8 GPUs
+        lo, hi = bounds[rank], bounds[rank + 1]
+        (s, i), (ulo, uhi) = sharded_score_topk(
+            torch.from_numpy(U), torch.from_numpy(I[lo:hi]), lo, k, group=lay.group,
+            local_topk=_local_topk_thr, merge=_merge_pad, n_items=I.shape[0], global_thr=True)
+        q.put((rank, ulo, uhi, s.numpy(), i.numpy(), distributed.LAST_FALLBACK_USERS))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("hot", [False, True])
+def test_item_sharded_8_ranks_global_thresholds_uneven(hot):
+    """World size 8 with global thresholds (the default 8-GPU path), k = 100
+    and an uneven contiguous item split (one shard shorter than k): merged
+    lists equal the single-process top-k. hot=True puts 40 hot rows at the
+    global sample positions (every 32nd row): the sample rank of the guess is
+    17 < 40 < k, so every non-negative user fails the guess and is recomputed
+    by the exact fallback."""
+    world, k = 8, 100
+    rng = np.random.default_rng(8100 + hot)
+    U = np.concatenate([rng.integers(0, 4, size=(15, 16)),
+                        rng.integers(-3, 4, size=(16, 16))]).astype(np.float32)
+    I = rng.integers(-3, 4, size=(6007, 16)).astype(np.float32)
+    if hot:
+        I[np.arange(40) * 32] = 3.0
+    bounds = [0, 40, 900, 1000, 2500, 2600, 4100, 5000, 6007]  # shard 0 has 40 < k rows
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, return_scores=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_thr8_worker, args=(r, world, port, U, I, k, bounds, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    owned = np.zeros(U.shape[0], dtype=int)
+    fb = set()
+    for rank, ulo, uhi, s, i, nfb in got:
+        assert (ulo, uhi) == shard_range(U.shape[0], world, rank)
+        assert np.array_equal(i, ref_i[ulo:uhi])
+        assert np.array_equal(s, ref_s[ulo:uhi].astype(np.float32))
+        owned[ulo:uhi] += 1
+        fb.add(nfb)
+    assert (owned == 1).all()
+    assert len(fb) == 1 and ((fb.pop() >= 15) if hot else True)
+
+
+def test_global_thresholds_need_n_items():
+    """global_thr without the whole catalog's row count fails before any
+    collective: a ValueError on every rank, not a hang."""
+    with pytest.raises(ValueError, match="n_items"):
+        sharded_score_topk(torch.zeros(3, 4), torch.zeros(10, 4), 0, 2, global_thr=True)
+    with pytest.raises(ValueError, match="n_items"):
+        sharded_score_topk(torch.zeros(3, 4), torch.zeros(10, 4), 5, 2, n_items=12, global_thr=True)

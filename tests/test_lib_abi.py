@@ -166,3 +166,40 @@ def test_seeded_topk_argument_errors_and_workspace():
     ws = lib.dr_score_topk_seeded_workspace(1_000_000, 1_250_000, bf16, 128, 100)
     assert ws >= (1_000_000 + 448) * 512 * 8
     assert lib.dr_score_topk_seeded_workspace(10, 10, bf16, 48, 10) == 0
+
+
+def test_headline_plans_on_a_256_cu_device():
+    """The plans of the benchmark shapes on 256 CUs (MI355X; this CPU host
+    reports no device, and the planner then assumes 256): the headline's
+    stride-128 guess with a 6-way split tail over the 4th round's 209 blocks,
+    config 2's two unsplit rounds at stride 32, the 8-way shard's stride 32,
+    and k = 1000's stride 32 (tests/test_real_plans.py runs them on the GPU)."""
+    if torch.cuda.is_available():
+        pytest.skip("plans depend on the device's CU count")
+    bf = torch.bfloat16
+    p = ops.score_topk_plan(1_000_000, 10_000_000, bf, 128, 100)
+    assert (p["users_per_wg"], p["user_blocks"], p["head_blocks"], p["tail_chunks"],
+            p["sample_stride"], p["sample_rank"]) == (1024, 977, 768, 6, 128, 10)
+    p = ops.score_topk_plan(1_000_000, 1_000_000, bf, 64, 100)
+    assert (p["users_per_wg"], p["user_blocks"], p["tail_chunks"], p["sample_stride"],
+            p["sample_rank"]) == (2048, 489, 1, 32, 17)
+    assert ops.score_topk_plan(1_000_000, 1_250_000, bf, 128, 100)["sample_stride"] == 32
+    assert ops.score_topk_plan(1_000_000, 5_000_000, bf, 128, 100)["sample_stride"] == 64
+    p = ops.score_topk_plan(1_000_000, 10_000_000, bf, 128, 1000)
+    assert (p["sample_stride"], p["cap"]) == (32, 2048)
+    assert ops.score_topk_plan(1000, 100_000, bf, 128, 100)["sample_stride"] == 0  # plain scan
+
+
+def test_distributed_stride_mirrors_the_planner():
+    """divrec.distributed.sample_stride (the global-threshold sample of the
+    item-sharded multi-GPU path) must pick the single-GPU guess's stride for
+    the whole catalog: compared with dr_score_topk_plan over catalog lengths
+    around every switch point and k below / above the long-list bound."""
+    from divrec.distributed import sample_stride
+
+    for n in (1 << 18, 1 << 20, 4_194_303, 4_194_304, 5_000_000, 8_388_607, 8_388_608,
+              10_000_000, 2 ** 23 + 1):
+        for k in (10, 100, 255, 256, 1000):
+            p = ops.score_topk_plan(4096, n, torch.bfloat16, 128, k)
+            if p["sample_stride"]:
+                assert sample_stride(n, k) == p["sample_stride"], (n, k)

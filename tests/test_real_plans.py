@@ -1,0 +1,236 @@
+"""The scan plans the benchmark configurations actually run, pinned against an
+exact reference.
+
+dr_score_topk picks its plan from the call's shape (csrc/score_topk.hip
+make_plan / guess_for): the sample stride of the guessed thresholds grows with
+the catalog (32 below 4.2M rows, 64 from 4.2M, 128 from 8.4M), and a grid whose
+last round would leave CUs idle splits its tail user blocks into catalog
+chunks. The headline (BASELINE configs[3] at one GPU: 1M users x 10M items,
+d = 128, k = 100) runs stride 128 with a 6-way split tail over 209 blocks;
+config 2 (1M x 1M, d = 64) runs stride 32 unsplit over two rounds. These tests
+run exactly those plans (asserted through dr_score_topk_plan) and compare the
+lists with the exact top-k, the reference's get_model_recommendations
+(/root/reference/divrec/train/utils.py:53-77) with its tie order fixed to
+(score desc, item id asc).
+
+Integer-valued tables make every score an exact integer in fp32 (|score| <=
+9 d), so the lists AND scores must be bit-identical; the reference scores are
+computed in float64 on the device (exact for these integers) and ranked by a
+stable descending sort over ascending item ids, which is the key order.
+
+* small shapes, planner knobs: DIVREC_GUESS_STRIDE 64 / 128 with
+  DIVREC_SCAN_SLOTS split plans, exclusions, duplicate user ids and "hot"
+  sample rows that make the guess fail for a user group (device-counted
+  rescan);
+* full size: 1M x 10M d = 128 k = 100 and 1M x 1M d = 64 k = 100, the calls
+  bench.py times, checked on ~1200 users drawn from head blocks, split-tail
+  blocks and the last partial block, plus an exclusion run and a hot-row
+  rescan group.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from divrec import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+class _Env:
+    """Set planner knobs (environment variables read at each dr_score_topk call)."""
+
+    def __init__(self, **kv):
+        self.kv = {k: str(v) for k, v in kv.items() if v is not None}
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def exact_topk_f64(U64: torch.Tensor, I64: torch.Tensor, k: int, frozen=None, block: int = 16):
+    """Exact (score desc, id asc) top-k of the rows of U64 over I64 (float64
+    device tensors holding integers: every score exact). frozen[r]: item ids
+    excluded for row r (scored -inf). Returns (items int64 [n, k], scores
+    float64 [n, k]) on the CPU."""
+    outi, outs = [], []
+    for b in range(0, U64.shape[0], block):
+        S = U64[b:b + block] @ I64.T
+        if frozen is not None:
+            for r in range(S.shape[0]):
+                f = frozen[b + r]
+                if len(f):
+                    S[r, torch.as_tensor(np.asarray(f, dtype=np.int64), device=S.device)] = -np.inf
+        kth = torch.topk(S, k, dim=1).values[:, -1]
+        for r in range(S.shape[0]):
+            cand = torch.nonzero(S[r] >= kth[r]).flatten()  # ascending ids
+            v, o = torch.sort(S[r, cand], descending=True, stable=True)
+            outi.append(cand[o[:k]].cpu())
+            outs.append(v[:k].cpu())
+        del S
+    return torch.stack(outi).numpy(), torch.stack(outs).numpy()
+
+
+def _int_table_dev(n, d, seed, lo=-3, hi=3):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return torch.randint(lo, hi + 1, (n, d), generator=g, device=DEV).to(torch.bfloat16)
+
+
+def _check(users_tab, items_tab, it, s, rows, k, frozen=None, user_ids=None):
+    """Compare output rows `rows` (positions) with the exact top-k."""
+    sel = rows if user_ids is None else user_ids[rows]
+    U64 = users_tab[torch.as_tensor(sel, device=DEV)].double()
+    I64 = items_tab.double()
+    fz = None if frozen is None else [frozen[r] for r in rows]
+    ref_i, ref_s = exact_topk_f64(U64, I64, k, fz)
+    del I64
+    got_i = it[torch.as_tensor(rows, device=DEV)].cpu().numpy().astype(np.int64)
+    got_s = s[torch.as_tensor(rows, device=DEV)].cpu().numpy()
+    bad = np.nonzero((got_i != ref_i).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size}/{len(rows)} users differ, first at position {rows[bad[0]]}"
+    assert np.array_equal(got_s, ref_s.astype(np.float32))
+
+
+# --------------------------------------------------------------------------- small shapes, forced plans
+@pytest.mark.parametrize("d,stride,slots", [(128, 128, 3), (128, 64, 3), (64, 128, None),
+                                            (64, 64, 2), (128, 128, None), (32, 64, 3)])
+def test_forced_stride_split_rescan_exact(d, stride, slots):
+    """Guess stride forced to 64 / 128 (the strides of >= 4.2M-row catalogs),
+    with and without a split-tail plan: integer tables, exclusions of some
+    users' best items, duplicate and permuted user ids, and 12 hot rows at
+    sample positions j * stride that are the best items of every non-negative
+    user (group A): the rank of the guess in the sample is < 12 for k = 50,
+    so A's threshold is the hot score, only the 12 hot items pass it and every
+    A user fails the guess and is rescanned. Lists and scores exact."""
+    rng = np.random.default_rng(d * 1000 + stride + (slots or 0))
+    upwg = 2048 if d <= 64 else 1024
+    ni, k = (1 << 18) + 777, 50
+    nu = (3 if slots else 1) * upwg + 333
+    half = nu // 2
+    U = np.concatenate([rng.integers(0, 4, size=(half, d)),
+                        rng.integers(-3, 4, size=(nu - half, d))]).astype(np.float32)
+    I = rng.integers(-3, 4, size=(ni, d)).astype(np.float32)
+    I[np.arange(12) * stride] = 3.0  # hot sample rows
+    users = np.concatenate([rng.permutation(nu), rng.integers(0, nu, 50)]).astype(np.int64)
+    frozen = [rng.choice(ni, size=int(rng.integers(0, 25)), replace=False) for _ in users]
+    for n in range(0, len(users), 53):  # exclude a hot row and some of the user's best items
+        best = np.argsort(-(I @ U[users[n]]), kind="stable")[:8]
+        frozen[n] = np.union1d(frozen[n], np.concatenate([best, [stride * 3]]))
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    Ub, Ib = torch.from_numpy(U).to(DEV).to(torch.bfloat16), torch.from_numpy(I).to(DEV).to(torch.bfloat16)
+    with _Env(DIVREC_GUESS_STRIDE=stride, DIVREC_SCAN_SLOTS=slots):
+        plan = ops.score_topk_plan(len(users), ni, torch.bfloat16, d, k)
+        s, it = ops.score_topk(Ub, Ib, k, user_ids=torch.from_numpy(users).to(DEV),
+                               exclude=(torch.from_numpy(rowptr).to(DEV),
+                                        torch.from_numpy(cols).to(DEV)))
+    assert plan["sample_stride"] == stride and plan["sample_rank"] < 12
+    if slots:
+        assert plan["tail_chunks"] > 1 and plan["head_blocks"] > 0
+    _check(Ub, Ib, it, s, np.arange(len(users)), k, frozen, users)
+
+
+def test_forced_stride_k1000_split():
+    """k = 1000 (config 5's candidate lists) keeps stride 32 by default; forced
+    to 64 with a split tail (long lists split in two): exact."""
+    rng = np.random.default_rng(31337)
+    d, ni, k = 128, (1 << 18) + 5, 1000
+    nu = 3 * 1024 + 17
+    U = rng.integers(-3, 4, size=(nu, d)).astype(np.float32)
+    I = rng.integers(-3, 4, size=(ni, d)).astype(np.float32)
+    Ub, Ib = torch.from_numpy(U).to(DEV).to(torch.bfloat16), torch.from_numpy(I).to(DEV).to(torch.bfloat16)
+    with _Env(DIVREC_GUESS_STRIDE=64, DIVREC_SCAN_SLOTS=2):
+        plan = ops.score_topk_plan(nu, ni, torch.bfloat16, d, k)
+        s, it = ops.score_topk(Ub, Ib, k)
+    assert plan["sample_stride"] == 64 and plan["tail_chunks"] == 2
+    rows = np.concatenate([np.arange(0, nu, 29), [nu - 1]])
+    _check(Ub, Ib, it, s, rows, k)
+
+
+# --------------------------------------------------------------------------- full size
+def _sample_rows(rng, plan, n_users, n_head, n_tail, n_last):
+    """Positions from head blocks, from split-tail blocks and from the last
+    (partial) user block, plus every block boundary around the head/tail cut."""
+    upwg = plan["users_per_wg"]
+    head_end = min(plan["head_blocks"] * upwg, n_users)
+    last0 = (plan["user_blocks"] - 1) * upwg
+    rows = [rng.choice(head_end, n_head, replace=False)]
+    if head_end < n_users:
+        rows.append(head_end + rng.choice(last0 - head_end, n_tail, replace=False))
+    rows.append(np.arange(max(last0, n_users - n_last), n_users))
+    edge = [0, upwg - 1, upwg, head_end - 1, head_end, head_end + upwg - 1, last0 - 1, last0,
+            n_users - 1]
+    rows.append(np.asarray([e for e in edge if 0 <= e < n_users]))
+    return np.unique(np.concatenate(rows))
+
+
+def test_headline_plan_1m_x_10m_exact():
+    """BASELINE configs[3] at one GPU, the call bench.py times: 1M users x 10M
+    items, d = 128, k = 100 — stride-128 guess, 6-way split tail over the 209
+    blocks of the 4th round. Integer tables generated on the device; 12 hot
+    rows at sample positions are the best items of a non-negative user group
+    spread over head and tail blocks (their guess fails: rescan). Checked: ~1200
+    users from head blocks, tail blocks and the last partial block, and 200 of
+    the hot group; then the same call with an exclusion CSR (the sampled users'
+    best items excluded)."""
+    U_n, I_n, d, k = 1_000_000, 10_000_000, 128, 100
+    plan = ops.score_topk_plan(U_n, I_n, torch.bfloat16, d, k)
+    assert (plan["sample_stride"], plan["tail_chunks"], plan["head_blocks"],
+            plan["user_blocks"]) == (128, 6, 768, 977), plan
+    rng = np.random.default_rng(2026)
+    users = _int_table_dev(U_n, d, 11)
+    items = _int_table_dev(I_n, d, 12)
+    items[torch.arange(12, device=DEV) * 128] = 3.0
+    hot = np.unique(rng.choice(U_n, 3000, replace=False))
+    hot_t = torch.as_tensor(hot, device=DEV)
+    users[hot_t] = users[hot_t].abs()  # non-negative rows: the hot items are their best
+    s, it = ops.score_topk(users, items, k)
+    rows = _sample_rows(rng, plan, U_n, 400, 500, 300)
+    _check(users, items, it, s, rows, k)
+    _check(users, items, it, s, rng.choice(hot, 200, replace=False), k)
+    # exclusions: each sampled user loses its exact top-10 and 20 random items
+    rows2 = rows[::3]
+    ref_i, _ = exact_topk_f64(users[torch.as_tensor(rows2, device=DEV)].double(), items.double(), 10)
+    frozen = [[] for _ in range(U_n)]
+    for r, best in zip(rows2, ref_i):
+        frozen[r] = np.union1d(best, rng.choice(I_n, 20, replace=False))
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    s2, it2 = ops.score_topk(users, items, k, exclude=(torch.from_numpy(rowptr).to(DEV),
+                                                       torch.from_numpy(cols).to(DEV)))
+    _check(users, items, it2, s2, rows2, k, frozen=frozen)
+    # users without exclusions get the same lists in the exclusion run
+    rest = torch.as_tensor(np.setdiff1d(rows, rows2), device=DEV)
+    assert torch.equal(it2[rest], it[rest]) and torch.equal(s2[rest], s[rest])
+
+
+def test_config2_plan_1m_x_1m_d64_exact():
+    """BASELINE configs[1], the call bench.py --workload score1m times: 1M x 1M,
+    d = 64, k = 100 — stride-32 guess, 489 user blocks of 2048 (two rounds,
+    unsplit). Integer tables; ~1200 users from both rounds and the last
+    partial block, and a hot-row rescan group."""
+    U_n, I_n, d, k = 1_000_000, 1_000_000, 64, 100
+    plan = ops.score_topk_plan(U_n, I_n, torch.bfloat16, d, k)
+    assert (plan["sample_stride"], plan["tail_chunks"], plan["user_blocks"]) == (32, 1, 489), plan
+    rng = np.random.default_rng(64)
+    users = _int_table_dev(U_n, d, 21)
+    items = _int_table_dev(I_n, d, 22)
+    # 20 hot rows at stride-32 sample positions; the guess's sample rank is 17
+    items[torch.arange(20, device=DEV) * 32] = 3.0
+    hot = np.unique(rng.choice(U_n, 3000, replace=False))
+    hot_t = torch.as_tensor(hot, device=DEV)
+    users[hot_t] = users[hot_t].abs()
+    s, it = ops.score_topk(users, items, k)
+    rows = np.unique(np.concatenate([_sample_rows(rng, plan, U_n, 500, 0, 300),
+                                     256 * 2048 + rng.choice(U_n - 256 * 2048, 400, replace=False)]))
+    _check(users, items, it, s, rows, k)
+    _check(users, items, it, s, rng.choice(hot, 200, replace=False), k)
