@@ -55,12 +55,14 @@ template <typename R, typename T, typename ACC>
 __global__ __launch_bounds__(256) void ild_dense_seq(const R* __restrict__ recs, int64_t n_users,
                                                      int k, const T* __restrict__ D,
                                                      int64_t n_items, float* __restrict__ out,
+                                                     double* __restrict__ raw,
                                                      int32_t* __restrict__ err) {
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (u >= n_users) return;
   const R* r = recs + u * k;
   if (!lane_list_ok(r, k, n_items)) {
-    out[u] = __builtin_nanf("");
+    if (raw) raw[u] = __builtin_nan("");
+    else out[u] = __builtin_nanf("");
     if (err) atomicAdd(err, 1);
     return;
   }
@@ -69,7 +71,8 @@ __global__ __launch_bounds__(256) void ild_dense_seq(const R* __restrict__ recs,
     const T* row = D + rec_at(r, p) * n_items;
     for (int q = p + 1; q < k; ++q) acc += row[rec_at(r, q)];
   }
-  out[u] = (float)acc / (float)(k * (k - 1));
+  if (raw) raw[u] = (double)acc;  // the pair sum in D's precision (user_ild)
+  else out[u] = (float)acc / (float)(k * (k - 1));
 }
 
 // --------------------------------------------------------------- dense, integer
@@ -77,6 +80,7 @@ template <typename R, typename T>
 __global__ __launch_bounds__(256) void ild_dense_int(const R* __restrict__ recs, int64_t n_users,
                                                      int k, const T* __restrict__ D,
                                                      int64_t n_items, float* __restrict__ out,
+                                                     double* __restrict__ raw,
                                                      int32_t* __restrict__ err) {
   const int lane = dr::lane_id();
   const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
@@ -84,7 +88,8 @@ __global__ __launch_bounds__(256) void ild_dense_int(const R* __restrict__ recs,
   const R* r = recs + u * k;
   if (!wave_list_ok(r, k, n_items)) {  // wave-uniform
     if (lane == 0) {
-      out[u] = __builtin_nanf("");
+      if (raw) raw[u] = __builtin_nan("");
+      else out[u] = __builtin_nanf("");
       if (err) atomicAdd(err, 1);
     }
     return;
@@ -96,7 +101,10 @@ __global__ __launch_bounds__(256) void ild_dense_int(const R* __restrict__ recs,
   }
 #pragma unroll
   for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
-  if (lane == 0) out[u] = (float)acc / (float)(k * (k - 1));
+  if (lane == 0) {
+    if (raw) raw[u] = (double)acc;  // exact while |sum| < 2^53
+    else out[u] = (float)acc / (float)(k * (k - 1));
+  }
 }
 
 // --------------------------------------------------------------- labels
@@ -380,30 +388,30 @@ int launch_embedding(const R* recs, int64_t n_users, int k, const __bf16* E, int
 
 template <typename R>
 int launch_dense(const R* recs, int64_t n_users, int k, const void* D, int dd, int64_t n_items,
-                 float* out, int32_t* err, hipStream_t s) {
+                 float* out, double* raw, int32_t* err, hipStream_t s) {
   switch (dd) {
     case DR_F32: {
       const int grid = (int)dr::ceil_div(n_users, 256);
       hipLaunchKernelGGL((ild_dense_seq<R, float, float>), grid, 256, 0, s, recs, n_users, k,
-                         (const float*)D, n_items, out, err);
+                         (const float*)D, n_items, out, raw, err);
       break;
     }
     case DR_F64: {
       const int grid = (int)dr::ceil_div(n_users, 256);
       hipLaunchKernelGGL((ild_dense_seq<R, double, double>), grid, 256, 0, s, recs, n_users, k,
-                         (const double*)D, n_items, out, err);
+                         (const double*)D, n_items, out, raw, err);
       break;
     }
     case DR_I32: {
       const int grid = (int)dr::ceil_div(n_users, 4);
       hipLaunchKernelGGL((ild_dense_int<R, int32_t>), grid, 256, 0, s, recs, n_users, k,
-                         (const int32_t*)D, n_items, out, err);
+                         (const int32_t*)D, n_items, out, raw, err);
       break;
     }
     case DR_I64: {
       const int grid = (int)dr::ceil_div(n_users, 4);
       hipLaunchKernelGGL((ild_dense_int<R, int64_t>), grid, 256, 0, s, recs, n_users, k,
-                         (const int64_t*)D, n_items, out, err);
+                         (const int64_t*)D, n_items, out, raw, err);
       break;
     }
     default:
@@ -424,9 +432,28 @@ extern "C" int dr_ild_dense(const void* recs, int rec_dtype, int64_t n_users, in
   DR_CHECK_ARG(recs && dist && out, "null pointer");
   hipStream_t s = (hipStream_t)stream;
   int rc = rec_dtype == DR_I32
-               ? launch_dense((const int32_t*)recs, n_users, k, dist, dist_dtype, n_items, out, err, s)
-               : launch_dense((const int64_t*)recs, n_users, k, dist, dist_dtype, n_items, out, err,
-                              s);
+               ? launch_dense((const int32_t*)recs, n_users, k, dist, dist_dtype, n_items, out,
+                              nullptr, err, s)
+               : launch_dense((const int64_t*)recs, n_users, k, dist, dist_dtype, n_items, out,
+                              nullptr, err, s);
+  if (rc != DR_OK) return rc;
+  DR_CHECK_LAUNCH();
+  return DR_OK;
+}
+
+extern "C" int dr_ild_dense_pair_sum(const void* recs, int rec_dtype, int64_t n_users, int k,
+                                     const void* dist, int dist_dtype, int64_t n_items,
+                                     double* out, int32_t* err, dr_stream_t stream) {
+  DR_CHECK_ARG(k >= 1, "k must be >= 1");
+  DR_CHECK_ARG(rec_dtype == DR_I32 || rec_dtype == DR_I64, "rec_dtype must be DR_I32/DR_I64");
+  if (n_users == 0) return DR_OK;
+  DR_CHECK_ARG(recs && dist && out, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  int rc = rec_dtype == DR_I32
+               ? launch_dense((const int32_t*)recs, n_users, k, dist, dist_dtype, n_items, nullptr,
+                              out, err, s)
+               : launch_dense((const int64_t*)recs, n_users, k, dist, dist_dtype, n_items, nullptr,
+                              out, err, s);
   if (rc != DR_OK) return rc;
   DR_CHECK_LAUNCH();
   return DR_OK;

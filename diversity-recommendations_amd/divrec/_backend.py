@@ -56,6 +56,7 @@ SIGNATURES = {
     ),
     "dr_topk_merge": (_i32, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p]),
     "dr_ild_dense": (_i32, [_p, _i32, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
+    "dr_ild_dense_pair_sum": (_i32, [_p, _i32, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "dr_ild_labels": (_i32, [_p, _i32, _i64, _i32, _p, _i64, _p, _p, _p]),
     "dr_ild_embedding": (_i32, [_p, _i32, _i64, _i32, _p, _i64, _i32, _i32, _p, _p, _p]),
     "dr_bpr_fwd_bwd": (_i32, [_p, _i64, _p, _i64, _i64, _p, _p, _p, _i64, _f32, _p, _p, _p, _p,

@@ -107,13 +107,18 @@ class IntraListDiversityScore(RecommendationsAwareLoss):
         return self.recommendations_loss(interactions, recommendations)
 
     @staticmethod
-    def user_ild(user_recommendations: torch.Tensor, distance_matrix: torch.Tensor) -> float:
-        """Un-normalised pair sum of one list (reference :36-42), on the GPU."""
+    def user_ild(user_recommendations: torch.Tensor, distance_matrix: torch.Tensor):
+        """Un-normalised pair sum of one list (reference :36-42): Python's
+        sum over itertools.combinations of 0-d tensors of D's dtype, i.e. a
+        0-d tensor of that dtype accumulated in order (int 0 for fewer than
+        two items). Computed by dr_ild_dense_pair_sum in D's own precision, so
+        the value is bit-identical; returned on D's device."""
         recs = user_recommendations.reshape(1, -1)
-        k = recs.size(1)
-        val = ops.ild_dense(recs.to(_backend.default_device()),
-                            distance_matrix.to(_backend.default_device()))
-        return float(val[0]) * k * (k - 1)
+        if recs.size(1) < 2:
+            return 0  # sum() of no pairs
+        dev = _backend.default_device()
+        val = ops.ild_dense_pair_sum(recs.to(dev), distance_matrix.to(dev))
+        return val[0].to(distance_matrix.dtype).to(distance_matrix.device)
 
 
 class IntraListBinaryUnfairnessScore(IntraListDiversityScore, DatasetAwareLoss):

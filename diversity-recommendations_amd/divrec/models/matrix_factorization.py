@@ -17,7 +17,9 @@ precisions:
   * ``"bf16"``: bf16 copies of the tables on the bf16 MFMA (16x the rate),
     ranking the tables' bf16 rounding — the explicit fast mode.
 Any ``embedding_dim`` works: widths without a scan instance (e.g. the
-reference experiments' 100) are zero-padded once per parameter version.
+reference experiments' 100) are zero-padded per call (a copy of O((U + I) d)
+bytes, small beside the O(U I d) scan; no cache, so writes through ``.data``
+or raw pointers, which bump no autograd version, are always seen).
 """
 from __future__ import annotations
 
@@ -74,7 +76,6 @@ class MatrixFactorization(RankingModel):
         self.embedding_dim = embedding_dim
         self.user_embeddings = torch.nn.Embedding(no_users, embedding_dim)
         self.item_embeddings = torch.nn.Embedding(no_items, embedding_dim)
-        self._tables = {}  # precision -> (key, user table, item table) for score_topk
 
     def _device(self) -> torch.device:
         dev = self.user_embeddings.weight.device
@@ -101,9 +102,9 @@ class MatrixFactorization(RankingModel):
     def scoring_tables(self, precision: str = "fp32") -> Tuple[torch.Tensor, torch.Tensor]:
         """The (user, item) tables score_topk scans at ``precision``: the
         parameters themselves when their dtype and width already have a scan
-        instance, else a converted / zero-padded copy, re-made only when a
-        parameter changed (keyed on storage and autograd version; the fused
-        optimizer steps bump the version, train/utils.py)."""
+        instance, else a converted / zero-padded copy made by this call (never
+        cached: an update through ``weight.data`` or a raw-pointer optimizer
+        bumps no version a cache could key on)."""
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
         self._device()
@@ -112,14 +113,9 @@ class MatrixFactorization(RankingModel):
         w = ops.score_width(dt, U.size(1))
         if dt == U.dtype and w == U.size(1) and U.is_contiguous() and I.is_contiguous():
             return U.detach(), I.detach()
-        key = (U.data_ptr(), U._version, I.data_ptr(), I._version, U.dtype)
-        hit = self._tables.get(precision)
-        if hit is None or hit[0] != key:
-            with torch.no_grad():
-                hit = (key, ops.pad_columns(U.detach().to(dt).contiguous(), w),
-                       ops.pad_columns(I.detach().to(dt).contiguous(), w))
-            self._tables[precision] = hit
-        return hit[1], hit[2]
+        with torch.no_grad():
+            return (ops.pad_columns(U.detach().to(dt).contiguous(), w),
+                    ops.pad_columns(I.detach().to(dt).contiguous(), w))
 
     def bf16_tables(self) -> Tuple[torch.Tensor, torch.Tensor]:
         """bf16 copies of both tables (the fast scoring mode's operands)."""

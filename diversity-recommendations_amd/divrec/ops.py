@@ -143,8 +143,9 @@ def score_topk(
     The tables' dtype picks the arithmetic: bf16 tables run the bf16 MFMA scan
     (exact products, fp32 sums: the fast mode), fp32 tables the fp32 MFMA scan
     (an exact fp32 fmaf chain per score: the reference's arithmetic up to the
-    summation order). Widths without a scan instance are zero-padded here (a
-    copy per call; MatrixFactorization caches its padded tables).
+    summation order). Widths without a scan instance are zero-padded here: a
+    copy of both tables on every call (O((U + I) d) bytes; pad once and pass
+    the padded tables when calling repeatedly on a large catalog).
 
     ``user_ids`` (int64) selects user rows; if None the first ``n_users`` rows
     (default: all) are scored. ``exclude = (rowptr int64 [n+1], items int32)``
@@ -281,6 +282,30 @@ def ild_dense(recs: torch.Tensor, dist: torch.Tensor) -> torch.Tensor:
     )
     B.check(rc, "dr_ild_dense")
     B.raise_if_out_of_range(err, "dr_ild_dense")
+    return out
+
+
+def ild_dense_pair_sum(recs: torch.Tensor, dist: torch.Tensor) -> torch.Tensor:
+    """Per-user UN-normalised pair sum sum_{p<q} D[r_p, r_q] (the reference's
+    user_ild), accumulated in D's precision; float64 [n] (exact for fp32 and
+    integer D)."""
+    dev = B.require_device(recs, dist)
+    recs, rc_dt = _recs(recs)
+    _need(dist.dim() == 2 and dist.size(0) == dist.size(1), "distance matrix must be [I, I]")
+    _need(dist.dtype in (torch.float32, torch.float64, torch.int32, torch.int64),
+          "distance matrix dtype must be float32/float64/int32/int64")
+    dist = dist.contiguous()
+    n, k = recs.shape
+    out = torch.empty(n, dtype=torch.float64, device=dev)
+    if n == 0:
+        return out
+    err = B.error_counter(dev)
+    rc = B.lib().dr_ild_dense_pair_sum(
+        recs.data_ptr(), rc_dt, n, k, dist.data_ptr(), B.dtype_code(dist.dtype), dist.size(0),
+        out.data_ptr(), err.data_ptr(), B.stream(dev),
+    )
+    B.check(rc, "dr_ild_dense_pair_sum")
+    B.raise_if_out_of_range(err, "dr_ild_dense_pair_sum")
     return out
 
 
@@ -484,7 +509,10 @@ def mmr_rerank(
     """Greedy MMR over per-user candidates (int32 [n, C] + fp32 [n, C]) -> int32 [n, k_out].
     Candidate ids < 0 are empty slots; with ``check`` an id >= the table's row
     count raises IndexError after the call (one counter read), as indexing the
-    table would (without it such candidates are silently never picked)."""
+    table would (without it such candidates are silently never picked).
+    Widths other than 64 / 128 are zero-padded HERE, on every call: a copy of
+    the whole table (multi-GB at 10M rows) — pad the table once and pass the
+    padded copy when calling repeatedly."""
     dev = B.require_device(cand_items, cand_scores, item_table)
     _need(cand_items.dtype == torch.int32 and cand_scores.dtype == torch.float32,
           "int32 candidate ids, fp32 scores")

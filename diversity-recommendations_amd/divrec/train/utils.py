@@ -101,6 +101,9 @@ def _list_length(dataset: RankingDataset, excl, n_users: int, n_items: int, k: i
     return lo
 
 
+MAX_SCAN_K = 1024  # dr_score_topk's largest k (include/divrec_hip.h)
+
+
 def get_model_recommendations(dataset: RankingDataset, model: RankingModel,
                               number_of_recommendations: int) -> torch.LongTensor:
     """Top-``number_of_recommendations`` candidates of every user of
@@ -116,9 +119,12 @@ def get_model_recommendations(dataset: RankingDataset, model: RankingModel,
         k_len = _list_length(dataset, excl, n_users, n_items, k)
         if k_len == 0:
             return torch.zeros((n_users, 0), dtype=torch.int64)
-        user_ids = None if n_users == model.no_users else torch.arange(n_users)
-        items, _ = model.score_topk(k_len, user_ids=user_ids, exclude=excl, n_items=n_items)
-        return items.cpu()
+        if k_len <= MAX_SCAN_K:
+            user_ids = None if n_users == model.no_users else torch.arange(n_users)
+            items, _ = model.score_topk(k_len, user_ids=user_ids, exclude=excl, n_items=n_items)
+            return items.cpu()
+        # lists longer than the scan's top-k bound: the loop below (the model's
+        # HIP forward per user, full sort), as the reference returns any length
     # Generic RankingModel: the reference loop (model scores per user), with
     # the deterministic tie-break. Outside the MF hot path.
     recs = []
@@ -192,8 +198,7 @@ def fused_adam_step(optimizer: torch.optim.Adam) -> None:
             ops.adam_dense(p.data, p.grad, st["exp_avg"], st["exp_avg_sq"], group["lr"], beta1,
                            beta2, group["eps"], group["weight_decay"], int(st["step"].item()))
             # the kernel wrote p through a raw pointer: bump its autograd
-            # version so caches keyed on it (MatrixFactorization's scoring
-            # tables) see the change, as after a torch in-place update
+            # version, as a torch in-place update would
             increment_version(p)
 
 
@@ -244,12 +249,13 @@ def pair_wise_train_loop(dataset: PairWiseDataset, model: RankingModel, loss: Pa
     fused = _bpr_fast_path(model, loss, scores)
     adam = _plain_adam(optimizer)
     lazy = fused and _plain_sparse_adam(optimizer)
-    epoch_err = None  # id range errors of the fused kernel, read once after the epoch
+    epoch_err = None  # id range errors of the fused kernel on device batches
     for user_id, pos, neg, uf, pf, nf in dataset.loader(**loader_params):
         if fused:
             dev = model._device()
             U, I = model.user_embeddings.weight, model.item_embeddings.weight
-            if user_id.device.type == "cpu":  # host batches: raise before any compute
+            host = user_id.device.type == "cpu"
+            if host:  # host batches: raise before any compute
                 _backend.host_ids_in_range(user_id, U.size(0), "user_id")
                 _backend.host_ids_in_range(pos, I.size(0), "positive item_id")
                 _backend.host_ids_in_range(neg, I.size(0), "negative item_id")
@@ -264,6 +270,12 @@ def pair_wise_train_loop(dataset: PairWiseDataset, model: RankingModel, loss: Pa
             losses_b, hits = ops.bpr_fwd_bwd(U.data, I.data, uid, pid, nid, 1.0 / B, U.grad, I.grad,
                                              err=epoch_err, check=False)
             loss_value = torch.sum(losses_b, dim=0) / B
+            if not host:
+                # device ids were range-checked by the kernel: read its counter
+                # (one sync) before the optimizer touches the parameters, so a
+                # bad batch raises IndexError with the model as the reference
+                # leaves it (nn.Embedding fails before any update)
+                _backend.raise_if_out_of_range(epoch_err, "pair_wise_train_loop")
             if lazy:  # touched rows only; the kernel zeroes those gradient rows
                 lazy_adam_step(optimizer, {U: torch.unique(uid),
                                            I: torch.unique(torch.cat([pid, nid]))})

@@ -169,6 +169,14 @@ int dr_topk_merge(const float* in_scores, const int32_t* in_items, int parts, in
 int dr_ild_dense(const void* recs, int rec_dtype, int64_t n_users, int k, const void* dist,
                  int dist_dtype, int64_t n_items, float* out, int32_t* err, dr_stream_t stream);
 
+/* The un-normalised pair sum of the same lists, sum_{p<q} D[r[u,p], r[u,q]], the
+ * reference's IntraListDiversityScore.user_ild (:36-42): accumulated in D's
+ * own precision in combinations order (fp32 D: the Python sum of 0-d fp32
+ * tensors, bit-exact; integer D: exact), stored as double (k = 1: 0). */
+int dr_ild_dense_pair_sum(const void* recs, int rec_dtype, int64_t n_users, int k,
+                          const void* dist, int dist_dtype, int64_t n_items, double* out,
+                          int32_t* err, dr_stream_t stream);
+
 /* Label equality D[i,j] = (label[i] == label[j]), the matrix of
  * IntraListBinaryUnfairnessScore.get_distance_matrix (:60-63), computed on the
  * fly from labels int64 [n_items] (exact integer count). */

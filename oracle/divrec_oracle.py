@@ -20,6 +20,7 @@ __all__ = [
     "topk_order",
     "topk_merge",
     "ild_sequential",
+    "ild_pair_sums",
     "ild_labels",
     "ild_embedding_f64",
     "embedding_distance_matrix",
@@ -149,13 +150,13 @@ def topk_merge(scores: np.ndarray, items: np.ndarray, k: int) -> Tuple[np.ndarra
     return out_s, out_i
 
 
-def ild_sequential(recs: np.ndarray, D: np.ndarray) -> np.ndarray:
-    """IntraListDiversityScore.recommendations_loss, reduction 'none'
-    (divrec/losses/intra_list_diversity_score.py:20-42): Python sum over
+def ild_pair_sums(recs: np.ndarray, D: np.ndarray) -> np.ndarray:
+    """IntraListDiversityScore.user_ild per list
+    (divrec/losses/intra_list_diversity_score.py:36-42): Python sum over
     itertools.combinations of positions, accumulated in D's dtype (fp32 for
-    fp32 D, exact for integer D), converted to fp32, divided by k*(k-1)."""
+    fp32 D, exact for integer D); 0 for fewer than two items. float64 [n]."""
     n, k = recs.shape
-    out = np.empty(n, dtype=np.float32)
+    out = np.empty(n, dtype=np.float64)
     is_int = np.issubdtype(D.dtype, np.integer)
     for u in range(n):
         acc = 0
@@ -163,7 +164,17 @@ def ild_sequential(recs: np.ndarray, D: np.ndarray) -> np.ndarray:
         for i, j in combinations(range(k), 2):
             v = D[row[i], row[j]]
             acc = acc + (int(v) if is_int else v)  # 0 + v == v exactly, then D-dtype adds
-        out[u] = np.float32(acc)
+        out[u] = acc
+    return out
+
+
+def ild_sequential(recs: np.ndarray, D: np.ndarray) -> np.ndarray:
+    """IntraListDiversityScore.recommendations_loss, reduction 'none'
+    (divrec/losses/intra_list_diversity_score.py:20-34): the user_ild pair
+    sums (ild_pair_sums) converted to fp32 by torch.Tensor, divided by
+    k*(k-1) in fp32."""
+    k = recs.shape[1]
+    out = ild_pair_sums(recs, D).astype(np.float32)
     with np.errstate(invalid="ignore", divide="ignore"):
         return (out / np.float32(k * (k - 1))).astype(np.float32)
 

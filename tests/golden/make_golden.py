@@ -140,8 +140,11 @@ def main():
             losses.IntraListDiversityScore(distance_matrix=D)(inter, recs)
         except IndexError:
             mean_raises = True
+        # user_ild (:36-42): the raw combinations sum per list (a 0-d fp32
+        # tensor; the int 0 of an empty sum for k = 1)
+        raw = np.asarray([float(ild.user_ild(row, D)) for row in recs], dtype=np.float32)
         save(f"ild_dense_k{k}", D=D, recs=recs, out=vals, sum=total,
-             mean_raises=np.bool_(mean_raises))
+             mean_raises=np.bool_(mean_raises), user_ild=raw)
 
     # label equality (IntraListBinaryUnfairnessScore with a 'partition' feature)
     labels = torch.randint(0, 3, (ni,), generator=g)

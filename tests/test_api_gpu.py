@@ -203,6 +203,41 @@ def test_scoring_tables_follow_fused_training():
         assert torch.equal(got, want), precision
 
 
+def test_get_model_recommendations_longer_than_scan_k():
+    """k > 1024 (beyond dr_score_topk): the reference returns lists of any
+    length (utils.py:53-77), so the MF path falls back to the per-user loop on
+    the model's HIP forward. Integer tables: exact against the oracle."""
+    rng = np.random.default_rng(1100)
+    nu, ni, d, k = 6, 1500, 16, 1100
+    U = rng.integers(-3, 4, size=(nu, d)).astype(np.float32)
+    I = rng.integers(-3, 4, size=(ni, d)).astype(np.float32)
+    tr = np.stack([np.repeat(np.arange(nu), 5), rng.integers(0, ni, nu * 5)], axis=1)
+    te = np.stack([np.arange(nu), rng.integers(0, ni, nu)], axis=1)
+    g = {"train": tr.astype(np.int64), "test": te.astype(np.int64)}
+    rds = ranking_dataset(g, nu, ni)
+    got = train.get_model_recommendations(rds, mf_from(U, I), k).numpy()
+    frozen = [np.unique(tr[tr[:, 0] == u, 1]) for u in range(nu)]
+    ref = oracle.recommend_topk(U, I, k, frozen=frozen)
+    assert got.shape == (nu, k) and np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_score_topk_sees_data_writes(precision):
+    """Writes through ``weight.data`` bump no autograd version:
+    ranking after such a write must use the new weights (d = 100: the padded
+    fp32 copy; bf16: the converted copy)."""
+    torch.manual_seed(5)
+    mf = models.MatrixFactorization(40, 300, 100).to(DEV)
+    before, _ = mf.score_topk(10, precision=precision)
+    mf.item_embeddings.weight.data.normal_()
+    mf.user_embeddings.weight.data.mul_(-1.0)
+    got, _ = mf.score_topk(10, precision=precision)
+    fresh = mf_from(mf.user_embeddings.weight.detach().cpu().numpy(),
+                    mf.item_embeddings.weight.detach().cpu().numpy())
+    want, _ = fresh.score_topk(10, precision=precision)
+    assert torch.equal(got, want) and not torch.equal(got, before)
+
+
 def test_pair_wise_train_loop_out_of_range_raises():
     """A batch with an item id outside the model's table: the reference's
     nn.Embedding raises IndexError; so does the fused loop (host batches are
@@ -286,6 +321,13 @@ def test_ild_dense_golden_bit_exact(k):
     if k > 1:
         s = losses.IntraListDiversityScore(distance_matrix=D, reduction="sum")(None, recs)
         assert float(s) == pytest.approx(float(g["sum"]), rel=1e-6)
+    # user_ild: the reference's raw combinations sum per list, bit-exact (0 for k = 1)
+    raw = [losses.IntraListDiversityScore.user_ild(row, D) for row in recs.cpu()]
+    if k == 1:
+        assert all(v == 0 for v in raw)
+    else:
+        assert all(v.dtype == D.dtype and v.dim() == 0 for v in raw)
+    assert np.array_equal(np.asarray([float(v) for v in raw], dtype=np.float32), g["user_ild"])
 
 
 def test_ild_labels_golden():

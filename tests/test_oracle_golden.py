@@ -66,6 +66,9 @@ def test_ild_dense_bit_exact(k):
     if k > 1:
         assert np.float32(np.sum(got.astype(np.float64))) == pytest.approx(float(g["sum"]), rel=1e-6)
     assert bool(g["mean_raises"])  # the reference's 'mean' forward raises IndexError
+    # user_ild: the raw pair sums, exactly the reference's values
+    assert np.array_equal(oracle.ild_pair_sums(g["recs"], g["D"]).astype(np.float32),
+                          g["user_ild"])
 
 
 def test_ild_labels_exact():
