@@ -116,7 +116,7 @@ def test_forced_stride_split_rescan_exact(d, stride, slots):
     rng = np.random.default_rng(d * 1000 + stride + (slots or 0))
     upwg = 2048 if d <= 64 else 1024
     ni, k = (1 << 18) + 777, 50
-    nu = (3 if slots else 1) * upwg + 333
+    nu = (slots or 1) * upwg + 333  # slots + 1 user blocks: one full round + a split tail
     half = nu // 2
     U = np.concatenate([rng.integers(0, 4, size=(half, d)),
                         rng.integers(-3, 4, size=(nu - half, d))]).astype(np.float32)
@@ -149,7 +149,7 @@ def test_forced_stride_k1000_split():
     U = rng.integers(-3, 4, size=(nu, d)).astype(np.float32)
     I = rng.integers(-3, 4, size=(ni, d)).astype(np.float32)
     Ub, Ib = torch.from_numpy(U).to(DEV).to(torch.bfloat16), torch.from_numpy(I).to(DEV).to(torch.bfloat16)
-    with _Env(DIVREC_GUESS_STRIDE=64, DIVREC_SCAN_SLOTS=2):
+    with _Env(DIVREC_GUESS_STRIDE=64, DIVREC_SCAN_SLOTS=3):  # 4 blocks: 3 head + a split tail
         plan = ops.score_topk_plan(nu, ni, torch.bfloat16, d, k)
         s, it = ops.score_topk(Ub, Ib, k)
     assert plan["sample_stride"] == 64 and plan["tail_chunks"] == 2
