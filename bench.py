@@ -1093,7 +1093,7 @@ def mmr_pipeline(args):
                         "kernel": f"dr_score_topk k={C} (the step's dominant kernel)"},
            "mmr_roofline": dict(_hbm(per_user * n_r, mmr_s,
                                      pmc_traffic("mmr", f"mmr_U{U_n}_I{I_n}_d{d}_C{C}_k{kout}",
-                                                 "mmr_batch_kernel") if world == 1 else None),
+                                                 "mmr_pick_kernel") if world == 1 else None),
                                 kernel="dr_mmr_rerank",
                                 per_unit=f"{per_user} B/user"),
            "cpu_baseline": cpu}

@@ -68,6 +68,15 @@ __device__ __forceinline__ uint32_t wave_min_u32_32(uint32_t v) {
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xA, 0xF, false));
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
 }
+__device__ __forceinline__ uint32_t wave_min_u32_64(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xA, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xC, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   v = dr::umax64(v, dpp_u64<0xB1>(v));        // quad_perm [1,0,3,2]
   v = dr::umax64(v, dpp_u64<0x4E>(v));        // quad_perm [2,3,0,1]
@@ -98,6 +107,26 @@ __device__ unsigned long long g_mmr_diag[kWaves][16];
 #endif
 enum { kMgLoad, kMgSelect, kMgStage, kMgMma, kMgSync1, kMgRounds, kMgSync2, kMgFold, kMgBatches,
        kMgTotal, kMgStageBar, kMgGt, kMgSlots = 16 };
+
+// Max of a float over the wave's 64 lanes by fused v_max_f32_dpp steps (one
+// VALU each), read from lane 63. -inf is the identity (bound_ctrl lanes read 0
+// and are masked by the row masks of the broadcast steps only, so the input
+// of every lane takes part; no NaN reaches here).
+__device__ __forceinline__ float wmax_f32(float v) {
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false)));
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false)));
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false)));
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false)));
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0x142, 0xA, 0xF, false)));
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0x143, 0xC, 0xF, false)));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
 
 // Max over the wave's 64 lanes (lanes = 64) or over lanes 0..31 (lanes = 32)
 // by fused v_max_u32_dpp steps (one VALU each: the reduction is the latency
@@ -131,6 +160,10 @@ __device__ __forceinline__ uint32_t wmax_u32(uint32_t v) {
 //   * per-candidate score, 1/|e| and id live in LDS (registers hold the rows
 //     and the columns).
 // Out-of-range ids (>= n_items) are counted in *err and never picked.
+#ifndef DR_MMR_LEGACY
+#define DR_MMR_LEGACY 0  // 1: the round-2 kernel below (A/B of the round-3 rewrite only)
+#endif
+#if DR_MMR_LEGACY
 template <int D>
 __global__ __launch_bounds__(kThreads) void mmr_batch_kernel(
     const int32_t* __restrict__ cand_items, const float* __restrict__ cand_scores, int C,
@@ -451,6 +484,423 @@ __global__ __launch_bounds__(kThreads) void mmr_batch_kernel(
     for (int i = 0; i < kMgSlots; ++i) atomicAdd(&g_mmr_diag[w][i], (unsigned long long)dg[i]);
 #endif
 }
+#endif  // DR_MMR_LEGACY
+
+// ---------------------------------------------------------------------------
+// Round-3 layout: MFMA work proportional to the PICKS, not to the probes.
+//   * 64 probes per batch (8 per wave) instead of 32: the bound (best value
+//     outside the probes) is lower, so more picks pass per batch (8 batches
+//     instead of 12 for 100 picks of real top-1000 lists, simulated);
+//   * the fast rounds need only the probes' pairwise cosines: a 64 x 64 Gram
+//     of the staged probe rows (4 MFMA tiles on waves 0-3) instead of 32
+//     columns of every candidate;
+//   * wave 0 holds its lane's Gram row in registers for the rounds (an SGPR-
+//     indexed register read instead of an LDS round trip per round);
+//   * after the rounds, ONE MFMA pass of the batch's picks (<= 32 rows per
+//     pass) against every candidate folds their columns into the max terms.
+// Exactness: the fold computes acc(pick p, candidate c) * inv|c| * inv|p| from
+// the same bf16 rows with the same operand roles (A = probe/pick rows from
+// LDS, B = candidate row) as the Gram, so the values the rounds see for a
+// probe are bit-identical to what the fold leaves in its max term: the picks
+// are exactly the eager greedy's on these fp32 cosines, as before.
+constexpr int kPP = 64;               // probes per batch
+constexpr int kPPW = kPP / kWaves;    // per wave
+typedef float f32x32 __attribute__((ext_vector_type(32)));
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
+    const int32_t* __restrict__ cand_items, const float* __restrict__ cand_scores, int C,
+    const __bf16* __restrict__ E, int64_t n_items, int k_out, float lambda,
+    int32_t* __restrict__ out_items, int32_t* __restrict__ err) {
+  constexpr int KS = D / 16;  // MFMA k-steps per row
+  constexpr int CPR = D / 8;  // 16-B chunks per row
+  constexpr int SWM = (CPR < 16 ? CPR : 16) - 1;
+  constexpr int GS = kPP + 4;  // s_g row stride in floats (16-B rows, 4 banks apart)
+  __shared__ uint4 s_prow[kPP * CPR];  // probe rows, chunk c of slot p at p*CPR + (c ^ (p & SWM))
+  // s_g[a*GS + p] = cos(probe a, probe p) rounded as a's fold would round it
+  __shared__ __attribute__((aligned(16))) float s_g[kPP * GS];
+  __shared__ float s_pinv[kPP], s_pscore[kPP], s_ppen[kPP];
+  __shared__ int s_pcand[kPP];   // candidate position of each probe slot (-1 = empty)
+  __shared__ int s_pitem[kPP];   // its item id
+  __shared__ int s_plist[kPP];   // this batch's picks: probe slots in pick order
+  __shared__ __attribute__((aligned(16))) float s_lpinv[kPP];  // 1/|e| of pick i
+  __shared__ int s_citem[kMaxC];
+  __shared__ float s_cscore[kMaxC], s_cinv[kMaxC];  // wave-local index cidx
+  __shared__ uint64_t s_wbound[kWaves];
+  __shared__ int s_state[4];  // rounds done, picks this batch, picked mask lo / hi
+  __shared__ int s_out[kMaxC];
+  auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  const int64_t u = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, q = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float mu = 1.f - lambda;
+  auto cpos = [&](int j) { return kWaves * (32 * j + q) + w; };
+  auto cidx = [&](int j) { return w * 128 + 32 * j + q; };
+#ifdef DR_MMR_DIAG
+  uint64_t dg[kMgSlots] = {};
+#endif
+  MG_T0(t_kernel);
+
+  // ---- candidate rows -> B fragments (as in the round-2 kernel)
+  bf16x8 brow[kTiles][KS];
+  float pen[kTiles];
+  uint32_t live = 0;
+  int nbad = 0;
+#pragma unroll
+  for (int j = 0; j < kTiles; ++j) {
+    const int c = cpos(j);
+    int32_t item = c < C ? cand_items[u * C + c] : -1;
+    if (item >= 0 && (int64_t)item >= n_items) {
+      nbad += h == 0 ? 1 : 0;
+      item = -1;
+    }
+    const bool ok = item >= 0;
+    live |= (ok ? 1u : 0u) << j;
+    const float sc = ok ? cand_scores[u * C + c] : 0.f;
+    if (h == 0) {
+      s_citem[c] = item;
+      s_cscore[cidx(j)] = sc;
+    }
+    pen[j] = -INFINITY;
+    const uint4* src = reinterpret_cast<const uint4*>(E + (int64_t)(ok ? item : 0) * D) + h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) brow[j][s] = __builtin_bit_cast(bf16x8, src[2 * s]);
+  }
+  if (nbad && err) atomicAdd(err, nbad);
+#pragma unroll
+  for (int j = 0; j < kTiles; ++j) {
+    float nsq = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const uint4 v = __builtin_bit_cast(uint4, brow[j][s]);
+      const uint32_t pr[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16x2 a = __builtin_bit_cast(bf16x2, pr[e]);
+        nsq = __builtin_amdgcn_fdot2_f32_bf16(a, a, nsq, false);
+      }
+    }
+    nsq += __shfl_xor(nsq, 32);
+    if (h == 0) s_cinv[cidx(j)] = 1.f / sqrtf(nsq);
+  }
+  __syncthreads();
+  MG_ADD(kMgLoad, t_kernel);
+
+  // Fold the np picks of s_plist (their rows staged in s_prow, 1/|e| in
+  // s_lpinv) into every candidate's max term: rows of A = the picks in pick
+  // order, 32 per pass; register r of tile j holds pick i = 8 (r / 4) + 4 h + r % 4.
+  auto fold = [&](int np, int h, int q) {
+    auto cidx = [&](int j) { return w * 128 + 32 * j + q; };
+    for (int i0 = 0; i0 < np; i0 += 32) {
+      const int nrow = np - i0 < 32 ? np - i0 : 32;
+      const int sq = q < nrow ? s_plist[i0 + q] : -1;
+      f32x16 acc[kTiles];
+#pragma unroll
+      for (int j = 0; j < kTiles; ++j) acc[j] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const uint4 av = sq >= 0 ? s_prow[sq * CPR + ((2 * s + h) ^ (sq & SWM))] : uint4{0, 0, 0, 0};
+        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+#pragma unroll
+        for (int j = 0; j < kTiles; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, brow[j][s], acc[j], 0, 0, 0);
+      }
+      float pv[16];
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const float4 v = *reinterpret_cast<const float4*>(&s_lpinv[i0 + 8 * gg + 4 * h]);
+        pv[4 * gg + 0] = v.x; pv[4 * gg + 1] = v.y; pv[4 * gg + 2] = v.z; pv[4 * gg + 3] = v.w;
+      }
+#pragma unroll
+      for (int j = 0; j < kTiles; ++j) {
+        const float ci = s_cinv[cidx(j)];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (8 * (r >> 2) + 4 * h + (r & 3) < nrow) mx = fmaxf(mx, acc[j][r] * ci * pv[r]);
+        pen[j] = fmaxf(pen[j], half_swap_max(mx));
+      }
+    }
+  };
+
+  // ---- first pick: the best live candidate by lambda * score (no max term
+  // yet), found by one wave max per wave + a combine; no probes, no rounds.
+  int t = 0;
+  {
+    uint64_t lk = 0ull;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = 2 * h + i;
+      if ((live >> j) & 1u) {
+        const float sc = s_cscore[cidx(j)];
+        lk = dr::umax64(lk, dr::make_key(lambda * sc, (uint32_t)cpos(j)));
+      }
+    }
+    const uint64_t wb = wave_max_u64(lk);
+    if (lane == 0) s_wbound[w] = wb;
+    lds_barrier();
+    uint64_t best = 0ull;
+#pragma unroll
+    for (int i = 0; i < kWaves; ++i) best = dr::umax64(best, s_wbound[i]);
+    if (best != 0ull) {
+      const int pc = (int)dr::key_item(best);
+      const int pj = (pc >> 3) >> 5, pq = (pc >> 3) & 31;
+      if (w == (pc & 7) && q == pq) {  // the owner lanes (both halves) stage its row
+#pragma unroll
+        for (int jj = 0; jj < kTiles; ++jj) {
+          if (jj == pj) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s) s_prow[(2 * s + h)] = __builtin_bit_cast(uint4, brow[jj][s]);
+          }
+        }
+        if (h == 0) {
+          s_plist[0] = 0;
+          s_lpinv[0] = s_cinv[w * 128 + 32 * pj + q];
+          s_out[0] = s_citem[pc];
+        }
+        live &= ~(1u << pj);
+      }
+      lds_barrier();
+      fold(1, h, q);
+      t = 1;
+    }
+    lds_barrier();  // s_wbound / s_prow are rewritten by the first batch
+  }
+  for (int batch = 0; t < k_out && batch <= k_out; ++batch) {
+    uint32_t tl = threadIdx.x;  // opaque lane coordinates (see mmr_batch_kernel)
+    asm volatile("" : "+v"(tl));
+    const int lane = (int)(tl & 63u), h = lane >> 5, q = lane & 31;
+    auto cpos = [&](int j) { return kWaves * (32 * j + q) + w; };
+    auto cidx = [&](int j) { return w * 128 + 32 * j + q; };
+    MG_T0(t_sel);
+
+    // ---- probes: the kPPW best live candidates of this wave + its bound, by
+    // the key order (value desc, position asc). Lane (q, h) ranks tiles 2h and
+    // 2h+1 (both half-waves hold the same candidates; this way each counts
+    // once) by the 32-bit value order ord(v) (0 = not live): one wave max per
+    // step; the candidate's position follows from its lane and tile, so the
+    // 64-bit key is needed only when two candidates tie on the value.
+    uint32_t v2[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float sc = s_cscore[w * 128 + 32 * (2 * h + i) + q];
+      uint32_t o = 0u;
+#pragma unroll
+      for (int j = 0; j < kTiles; ++j) {
+        if (j == 2 * h + i && ((live >> j) & 1u)) {
+          const float val = t == 0 ? lambda * sc : fmaf(-mu, pen[j], lambda * sc);
+          o = dr::f32_to_ord(val);
+        }
+      }
+      v2[i] = o;
+    }
+    uint32_t myslot = 0u;  // per tile j: probe slot + 1 of this lane's candidate (bits 8j..)
+#pragma unroll
+    for (int m = 0; m <= kPPW; ++m) {
+      const uint32_t mh = wmax_u32<64>(v2[0] > v2[1] ? v2[0] : v2[1]);
+      uint64_t best = 0ull;  // key of the m-th best candidate (0 = none)
+      int bl = -1, bi = 0;   // its lane and register (0: tile 2h, 1: tile 2h+1)
+      if (mh != 0u) {
+        const uint64_t b0 = __ballot(v2[0] == mh), b1 = __ballot(v2[1] == mh);
+        if (__popcll(b0) + __popcll(b1) == 1) {
+          bi = b0 ? 0 : 1;
+          bl = __builtin_ctzll(b0 | b1);
+        } else {  // equal values: lowest position wins (exact 64-bit keys)
+          uint64_t lk = 0ull;
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int pos = kWaves * (32 * (2 * h + i) + q) + w;
+            const uint64_t key = v2[i] == mh ? ((uint64_t)mh << 32) | (uint32_t)~pos : 0ull;
+            lk = dr::umax64(lk, key);
+          }
+          const uint64_t kb = wave_max_u64(lk);
+          const int pos = (int)dr::key_item(kb);
+          const int pq = (pos >> 3) & 31, pj = (pos >> 3) >> 5;
+          bl = pq + 32 * (pj >> 1);
+          bi = pj & 1;
+        }
+        const int pj = 2 * (bl >> 5) + bi;
+        const int pos = kWaves * (32 * pj + (bl & 31)) + w;
+        best = ((uint64_t)mh << 32) | (uint32_t)~pos;
+      }
+      if (m == kPPW) {
+        if (lane == 0) s_wbound[w] = best;
+        break;
+      }
+      const int slot = w * kPPW + m;
+      int pc = -1;
+      if (best != 0ull) {
+        pc = (int)dr::key_item(best);
+        if (lane == bl) v2[bi] = 0u;
+        const int pj = (pc >> 3) >> 5, pq = (pc >> 3) & 31;
+        if (q == pq) myslot |= (uint32_t)(slot + 1) << (8 * pj);
+      }
+      if (lane == 0) s_pcand[slot] = pc;
+    }
+    MG_ADD(kMgSelect, t_sel);
+    MG_T0(t_stage);
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j) {
+      const int sl = (int)((myslot >> (8 * j)) & 255u) - 1;
+      if (sl >= 0) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          s_prow[sl * CPR + ((2 * s + h) ^ (sl & SWM))] = __builtin_bit_cast(uint4, brow[j][s]);
+        if (h == 0) {
+          s_pitem[sl] = s_citem[cpos(j)];
+          s_pinv[sl] = s_cinv[cidx(j)];
+          s_pscore[sl] = s_cscore[cidx(j)];
+          s_ppen[sl] = pen[j];
+        }
+      }
+    }
+    MG_T0(t_sbar);
+    lds_barrier();
+    MG_ADD(kMgStageBar, t_sbar);
+    MG_ADD(kMgStage, t_stage);
+    MG_T0(t_mma);
+    if (w < 4) {
+      // Gram tile of waves 0-3: B columns = probes a = 32 ab + q, A rows =
+      // probes p = 32 pb + 8 (r / 4) + 4 h + r % 4 (register r)
+      const int pb = w & 1, ab = w >> 1;
+      const int ra = 32 * pb + q, rb = 32 * ab + q;
+      f32x16 g = f32x16{};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, s_prow[ra * CPR + ((2 * s + h) ^ (ra & SWM))]);
+        const bf16x8 b = __builtin_bit_cast(bf16x8, s_prow[rb * CPR + ((2 * s + h) ^ (rb & SWM))]);
+        g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, g, 0, 0, 0);
+      }
+      const float ci = s_pinv[rb];
+      float* row = &s_g[rb * GS + 32 * pb + 4 * h];
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const float4 v = *reinterpret_cast<const float4*>(&s_pinv[32 * pb + 8 * gg + 4 * h]);
+        const float pv[4] = {v.x, v.y, v.z, v.w};
+        float4 o;
+        o.x = g[4 * gg + 0] * ci * pv[0];
+        o.y = g[4 * gg + 1] * ci * pv[1];
+        o.z = g[4 * gg + 2] * ci * pv[2];
+        o.w = g[4 * gg + 3] * ci * pv[3];
+        *reinterpret_cast<float4*>(&row[8 * gg]) = o;
+      }
+    }
+    MG_ADD(kMgGt, t_mma);
+    MG_T0(t_sync1);
+    lds_barrier();
+    MG_ADD(kMgSync1, t_sync1);
+    MG_T0(t_rounds);
+    uint64_t bound = 0ull;
+#pragma unroll
+    for (int i = 0; i < kWaves; ++i) bound = dr::umax64(bound, s_wbound[i]);
+
+    // ---- fast rounds over the 64 probes on wave 0 (lane a = probe slot a).
+    // The chain of a round: value -> wave max (fused v_max_f32_dpp) -> ballot
+    // -> pick -> Gram entry (SGPR-indexed register read) -> max term. The
+    // round's outputs are kept in registers (lane i: output i of this batch)
+    // and written to LDS once after the rounds, so no LDS access, and no wait
+    // on one, sits in the chain.
+    if (w == 0) {
+      const int pa = s_pcand[lane];
+      const float lsa = lambda * s_pscore[lane];
+      float pna = s_ppen[lane];
+      f32x32 g0, g1;  // this probe's Gram row, indexed by the (uniform) pick slot
+      {
+        const float4* src = reinterpret_cast<const float4*>(&s_g[lane * GS]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float4 a = src[i], b = src[8 + i];
+          g0[4 * i + 0] = a.x; g0[4 * i + 1] = a.y; g0[4 * i + 2] = a.z; g0[4 * i + 3] = a.w;
+          g1[4 * i + 0] = b.x; g1[4 * i + 1] = b.y; g1[4 * i + 2] = b.z; g1[4 * i + 3] = b.w;
+        }
+      }
+      // values in the key order's high word: ord(v) (0 = not live)
+      auto ordv = [](float v) {
+        const uint32_t u = __float_as_uint(v + 0.0f);  // -0 -> +0
+        return u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+      };
+      const uint32_t bhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bound >> 32));
+      const uint32_t blo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bound);
+      // t >= 1 here whenever a live candidate exists (the first pick is made
+      // before the batches), so every live max term is finite
+      bool alive = pa >= 0;
+      uint32_t cur = alive ? ordv(fmaf(-mu, pna, lsa)) : 0u;
+      int rec_slot = -1;  // lane i: probe slot of pick i of this batch
+      const int t0 = t, nr = k_out - t;
+      int np = 0;
+      uint64_t picked = 0;
+      uint32_t m = 0u;
+      for (;;) {
+        m = wmax_u32<64>(cur);
+        if (m == 0u) break;  // no live probe: a non-probe is next, or nothing is left
+        uint64_t bal = __ballot(cur == m);
+        if (bal & (bal - 1)) {  // equal values: lowest candidate position wins
+          const uint32_t mp = wave_min_u32_64(cur == m ? (uint32_t)pa : 0xffffffffu);
+          bal = __ballot(cur == m && (uint32_t)pa == mp);
+        }
+        const int pk = __builtin_amdgcn_readfirstlane(__builtin_ctzll(bal));
+        const uint32_t npos = ~(uint32_t)__builtin_amdgcn_readlane(pa, pk);
+        // stop when a non-probe may be better, or the list is full
+        if (m < bhi || (m == bhi && npos <= blo) || np == nr) break;
+        const float ga = g0[pk & 31], gb = g1[pk & 31];
+        const float g = pk < 32 ? ga : gb;
+        rec_slot = lane == np ? pk : rec_slot;
+        picked |= 1ull << pk;
+        ++np;
+        alive = alive && lane != pk;
+        pna = g > pna ? g : pna;  // a select: fmaxf would canonicalize both inputs first
+        cur = alive ? ordv(fmaf(-mu, pna, lsa)) : 0u;
+      }
+      t += np;
+      if (lane < np) {
+        s_out[t0 + lane] = s_pitem[rec_slot];
+        s_plist[lane] = rec_slot;
+        s_lpinv[lane] = s_pinv[rec_slot];
+      }
+      if (m == 0u && (bhi | blo) == 0u) {  // no live candidate left: the rest are -1
+        for (int i = t + lane; i < k_out; i += 64) s_out[i] = -1;
+        t = k_out;
+      }
+      if (lane == 0) {
+        s_state[0] = t;
+        s_state[1] = np;
+        s_state[2] = (int)(uint32_t)picked;
+        s_state[3] = (int)(uint32_t)(picked >> 32);
+      }
+    }
+    MG_ADD(kMgRounds, t_rounds);
+    MG_T0(t_sync2);
+    lds_barrier();
+    t = s_state[0];
+    const int np = s_state[1];
+    const uint64_t picked = (uint64_t)(uint32_t)s_state[2] | ((uint64_t)(uint32_t)s_state[3] << 32);
+    MG_ADD(kMgSync2, t_sync2);
+    MG_T0(t_fold);
+
+    // ---- fold: the picks (rows of A, in pick order, 32 per pass) against
+    // every candidate
+    fold(np, h, q);
+    // picked probes of this wave leave the live set
+#pragma unroll
+    for (int j = 0; j < kTiles; ++j) {
+      const int sl = (int)((myslot >> (8 * j)) & 255u) - 1;
+      if (sl >= 0 && ((picked >> sl) & 1ull)) live &= ~(1u << j);
+    }
+    lds_barrier();  // LDS probe state is rewritten by the next batch
+    MG_ADD(kMgFold, t_fold);
+#ifdef DR_MMR_DIAG
+    dg[kMgBatches] += 1;
+#endif
+  }
+  __syncthreads();
+  for (int i = tid; i < k_out; i += kThreads) out_items[u * k_out + i] = s_out[i];
+#ifdef DR_MMR_DIAG
+  MG_ADD(kMgTotal, t_kernel);
+  if (lane == 0)
+    for (int i = 0; i < kMgSlots; ++i) atomicAdd(&g_mmr_diag[w][i], (unsigned long long)dg[i]);
+#endif
+}
 
 #ifdef DR_MMR_DIAG
 }  // namespace
@@ -479,8 +929,13 @@ extern "C" int dr_mmr_rerank(const int32_t* cand_items, const float* cand_scores
   DR_CHECK_ARG(cand_items && cand_scores && item_table && out_items, "null pointer");
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)n_users);
+#if DR_MMR_LEGACY
+#define DR_MMR_KERNEL mmr_batch_kernel
+#else
+#define DR_MMR_KERNEL mmr_pick_kernel
+#endif
 #define DR_MMR(DD)                                                                            \
-  hipLaunchKernelGGL(mmr_batch_kernel<DD>, grid, dim3(kThreads), 0, s, cand_items, cand_scores, \
+  hipLaunchKernelGGL(DR_MMR_KERNEL<DD>, grid, dim3(kThreads), 0, s, cand_items, cand_scores,    \
                      C, (const __bf16*)item_table, n_items, k_out, lambda, out_items, err)
   switch (d) {
     case 64: DR_MMR(64); break;

@@ -45,7 +45,7 @@ enum dr_ild_kind {
 /* Library version (major*10000 + minor*100 + patch). */
 int dr_version(void);
 /* Build id: the first 16 hex digits of a sha256 over the library's source files
- * (csrc/*.hip, csrc/*.h, include/*.h), baked in at compile time, so a run can
+ * (the .hip and .h files of csrc/ and include/), baked in at compile time, so a run can
  * show which sources the loaded library was built from. */
 const char* dr_build_id(void);
 /* Thread-local message of the last failing call on this thread ("" if none). */

@@ -67,7 +67,8 @@ def main():
     for t in tags:
         med = statistics.median(times[t])
         res["variants"][t] = {"median_ms": med, "users_per_s": args.users / med * 1e3,
-                              "identical": bool(torch.equal(outs[t], outs[tags[0]]))}
+                              "identical": bool(torch.equal(outs[t], outs[tags[0]])),
+                              "users_differ": int((outs[t] != outs[tags[0]]).any(dim=1).sum())}
     print(json.dumps(res), flush=True)
 
 
