@@ -313,12 +313,21 @@ def pmc_mfma(workload: str, config: str, kernel: str = "score_scan_kernel"):
         return None
     if rec.get("config") != config:
         return None
-    k = rec.get("kernels", {}).get(kernel)
+    ks = rec.get("kernels", {})
+    k = ks.get(kernel)
     if not k:
         return None
-    return {"mfma_busy_frac": k["mfma_busy_frac"], "effective_clock_ghz": k.get("clock_ghz"),
-            "mfma_busy_cycles": k["mfma_busy_cycles"], "simd_cycles": k["simd_cycles"],
-            "source": f"profiles/pmc_mfma_{workload}.json ({k.get('counters', 'SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE')})"}
+    # the instantiation with the most MFMA work (the seeded main scan)
+    inst = max((n for n in ks if n.startswith(kernel + "<")),
+               key=lambda n: ks[n]["mfma_busy_cycles"], default=None)
+    out = {"mfma_busy_frac": k["mfma_busy_frac"], "effective_clock_ghz": k.get("clock_ghz"),
+           "mfma_busy_cycles": k["mfma_busy_cycles"], "simd_cycles": k["simd_cycles"],
+           "busy_over_flops": k.get("busy_over_expected"),
+           "scope": f"every {kernel} dispatch of one call (sample scan, seeded scan, rescan)",
+           "source": f"profiles/pmc_mfma_{workload}.json ({k.get('counters')})"}
+    if inst:
+        out["main_scan"] = {"kernel": inst, "mfma_busy_frac": ks[inst]["mfma_busy_frac"]}
+    return out
 
 
 def provenance() -> dict:
@@ -590,16 +599,23 @@ def secondary(args):
         if want_cpu:
             import oracle
 
-            # bounded sample (~10 s of CPU work): users one at a time until the budget
-            Uh, Ih = users[:256].float().cpu().numpy(), items.float().cpu().numpy()
+            # the reference's per-user loop restated in torch (as the headline's
+            # baseline) on this process's CPU share, users one at a time until
+            # the budget (~10 s of CPU work)
+            threads, visible, model = host_cpu()
+            torch.set_num_threads(threads)
+            Uh, Ih = users[:256].float().cpu(), items.float().cpu()
+            oracle.reference_loop_topk(Uh, Ih, k, users=[0])  # warm
             n, t0 = 0, time.perf_counter()
             while n < 256 and time.perf_counter() - t0 < args.cpu_budget_s * 2 / 3:
-                oracle.recommend_topk(Uh, Ih, k, users=[n])
+                oracle.reference_loop_topk(Uh, Ih, k, users=[n])
                 n += 1
             t = time.perf_counter() - t0
-            cpu = {"value": n * I_n / t, "unit": "scored pairs/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle.recommend_topk (reference per-user loop), {n} users x "
-                             f"{I_n} items, {t:.1f}s"}
+            cpu = {"value": n * I_n / t, "unit": "scored pairs/s", "cores": threads,
+                   "kind": "port", "cpu_model": model, "cpus_visible": visible,
+                   "sample": f"oracle.reference_loop_topk (the reference get_model_recommendations "
+                             f"loop restated in torch), {n} users x {I_n} items, {t:.1f}s on "
+                             f"{threads} threads"}
         _line("scored pairs/sec, 1M x 1M d=64 top-100 (BASELINE configs[1])", U_n * I_n / wall,
               "scored pairs/s", args, wall, "bf16",
               {"workload": "score_topk 1M users x 1M items d=64 k=100", "users": U_n,
@@ -686,14 +702,20 @@ def secondary(args):
         if want_cpu:
             import oracle
 
-            Uh, Ih = Ut.cpu().numpy(), It.cpu().numpy()
-            m = 1 << 20
-            uh, ih = uid[:m].cpu().numpy(), iid[:m].cpu().numpy()
+            threads, visible, model = host_cpu()
+            torch.set_num_threads(threads)
+            Uh, Ih = Ut.cpu(), It.cpu()
+            m = 1 << 22
+            uh, ih = uid[:m].cpu(), iid[:m].cpu()
+            oracle.reference_mf_forward(Uh, Ih, uh[:4096], ih[:4096])  # warm
             t0 = time.perf_counter()
-            oracle.mf_forward(Uh, Ih, uh, ih)
+            oracle.reference_mf_forward(Uh, Ih, uh, ih)
             t = time.perf_counter() - t0
-            cpu = {"value": m / t, "unit": "pairs/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle.mf_forward (numpy gather + fp32 row sum), {m} pairs, {t:.2f}s"}
+            cpu = {"value": m / t, "unit": "pairs/s", "cores": threads, "kind": "port",
+                   "cpu_model": model, "cpus_visible": visible,
+                   "sample": f"oracle.reference_mf_forward (MatrixFactorization.forward restated "
+                             f"in torch: two embedding gathers + sum(u * i)), {m} uniform pairs, "
+                             f"{t:.2f}s on {threads} threads"}
         # the reference's own call patterns (runs of equal ids, each row read
         # once per run): RankingDataset's (full((n,), u), candidates) over the
         # whole catalog for 8 users, and PairWiseDataset's m x m product
@@ -868,22 +890,30 @@ def secondary(args):
         if want_cpu:
             import oracle
 
-            m = 8192
-            Uh, Ih = Ut.cpu().numpy(), It.cpu().numpy()
-            sl = [t_[:m].cpu().numpy() for t_ in (uid, pid, nid)]
-            t0 = time.perf_counter()
-            oracle.bpr_forward_backward(Uh, Ih, *sl)
-            t_fb = time.perf_counter() - t0
-            n_adam = 1 << 22
-            p0 = Uh.reshape(-1)[:n_adam]
-            t0 = time.perf_counter()
-            oracle.adam_step(p0, p0, np.zeros_like(p0), np.zeros_like(p0), 1)
-            t_adam = (time.perf_counter() - t0) * (2 * U_n * d) / n_adam
-            cpu_step = t_fb * B / m + t_adam
-            cpu = {"value": B / cpu_step, "unit": "triples/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle.bpr_forward_backward on {m} triples ({t_fb:.2f}s, x{B // m}) + "
-                             f"oracle.adam_step on {n_adam} of {2 * U_n * d} params "
-                             f"(extrapolated {t_adam:.1f}s): {cpu_step:.0f}s per step"}
+            # one pair_wise_train_loop batch restated in torch (two MF forwards,
+            # LogSigmoidDifferenceLoss, backward into dense embedding gradients,
+            # Adam over both 1M x 128 tables) on this process's CPU share, at
+            # two batch sizes: step time = fixed (Adam + zero_grad over the
+            # tables) + per-triple part, extrapolated to the batch of B
+            threads, visible, model = host_cpu()
+            torch.set_num_threads(threads)
+            Uh, Ih = Ut.cpu(), It.cpu()
+            bs = (1 << 15, 1 << 16)
+            ts = []
+            for b_ in bs:
+                bt = [tuple(t_[:b_].cpu() for t_ in (uid, pid, nid))]
+                t0 = time.perf_counter()
+                oracle.reference_bpr_steps(Uh, Ih, bt)
+                ts.append(time.perf_counter() - t0)
+            per = max((ts[1] - ts[0]) / (bs[1] - bs[0]), 0.0)
+            fixed = max(ts[0] - per * bs[0], 0.0)
+            cpu_step = fixed + per * B
+            cpu = {"value": B / cpu_step, "unit": "triples/s", "cores": threads, "kind": "port",
+                   "cpu_model": model, "cpus_visible": visible,
+                   "sample": f"oracle.reference_bpr_steps (the reference's BPR batch restated in "
+                             f"torch: forwards, loss, backward, Adam.step) at {bs[0]} and {bs[1]} "
+                             f"triples on the full tables ({ts[0]:.1f}s, {ts[1]:.1f}s) on "
+                             f"{threads} threads, extrapolated to {B}: {cpu_step:.1f}s per step"}
         _line("BPR training triples/sec, 1M x 1M d=128 (BASELINE configs[2])", B / wall,
               "triples/s", args, wall, "f32",
               {"workload": f"one BPR step: dr_bpr_fwd_bwd over {B} triples (uniform user, "
@@ -1064,14 +1094,20 @@ def mmr_pipeline(args):
         sys.path.insert(0, ROOT)
         import oracle
 
-        m = 4
-        Eh = items.float().cpu().numpy()
+        threads, visible, model = host_cpu()
+        torch.set_num_threads(threads)
+        m = 64
+        Eh = items.float().cpu()
+        ci, cs = out["cand"][:m].cpu(), out["sc"][:m].cpu()
+        oracle.mmr_greedy_torch(ci[:1], cs[:1], Eh, kout, lam)  # warm
         t1 = time.perf_counter()
-        oracle.mmr_greedy(out["cand"][:m].cpu().numpy(), out["sc"][:m].cpu().numpy(), Eh, kout, lam)
+        oracle.mmr_greedy_torch(ci, cs, Eh, kout, lam)
         tm = time.perf_counter() - t1
-        cpu = {"value": m / tm, "unit": "users/s (MMR re-rank only)", "cores": 1, "kind": "port",
-               "sample": f"oracle.mmr_greedy (float64 numpy) on the first {m} users' real "
-                         f"top-{C} lists, {tm:.2f}s"}
+        cpu = {"value": m / tm, "unit": "users/s (MMR re-rank only)", "cores": threads,
+               "kind": "port", "cpu_model": model, "cpus_visible": visible,
+               "sample": f"oracle.mmr_greedy_torch (the eager greedy in torch fp32: one C x C "
+                         f"cosine GEMM + {kout} argmax rounds per user) on the first {m} users' "
+                         f"real top-{C} lists, {tm:.2f}s on {threads} threads"}
     rec = {"metric": f"MMR pipeline users/sec: top-{C} of {I_n} items -> MMR top-{kout} -> ILD, "
                      f"d={d} (BASELINE configs[4])",
            "value": U_n / step_s, "unit": "users/s", "n_gpus": world, "steps": args.steps,

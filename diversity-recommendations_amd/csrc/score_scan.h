@@ -571,6 +571,12 @@ struct TopkArgs {
   int slack;            // keys a compaction keeps beyond k (kSlack; smaller for sample scans)
   int gap;              // new keys a buffer takes past k + slack before it is compacted
   const float* init_thr;  // [n_users_pad] starting thresholds (SEEDED scans only)
+  // Second-tier rescan only (dev_split > 0): the user count is on the device,
+  // so the grid's units are planned there: every user block is split into up
+  // to dev_split catalog chunks (dev_split_plan), chunk buffers past the
+  // blocks' chunk-0 rows, bounded by buf_blocks user blocks of buffer rows.
+  int dev_split;
+  int64_t buf_blocks;
   // Fallback rescan only: the user count lives on the device (n_users and
   // n_ublocks above are its upper bounds), and pos_map[p] is the caller's
   // position of list entry p (its exclusion row). NULL otherwise.
@@ -580,6 +586,35 @@ struct TopkArgs {
   int32_t* cnt;    // [buffer rows] valid keys per buffer
   uint64_t* diag;  // [gridDim.x * kWaves][kDgSlots] in DR_TOPK_DIAG builds
 };
+
+// Chunking of a second-tier rescan, computed where the failing-user count is
+// (on the device; the scan and its finalize compute the same plan): nb user
+// blocks share `grid` workgroups, so each block's catalog is split into
+// c ~ grid / nb chunks (at most max_c, at least min_chunk rows each, and no
+// more chunk buffers than buf_blocks blocks of rows hold); chunk length is a
+// whole number of stages.
+struct DevSplit {
+  int chunks;
+  int64_t chunk_items;
+};
+__host__ __device__ inline DevSplit dev_split_plan(int64_t nb, int64_t grid, int max_c,
+                                                   int64_t buf_blocks, int64_t n_items,
+                                                   int64_t stage_items) {
+  constexpr int64_t kMinChunk = 16384;
+  int64_t c = nb > 0 ? grid / nb : 1;
+  c = c < max_c ? c : max_c;
+  const int64_t by_buf = nb > 0 ? buf_blocks / nb : 1;
+  c = c < by_buf ? c : by_buf;
+  const int64_t by_len = n_items / kMinChunk;
+  c = c < by_len ? c : by_len;
+  if (c < 1) c = 1;
+  int64_t per = (n_items + c - 1) / c;
+  per = (per + stage_items - 1) / stage_items * stage_items;
+  DevSplit d;
+  d.chunk_items = per;
+  d.chunks = (int)((n_items + per - 1) / per);
+  return d;
+}
 
 template <int W, int CAP, bool SEEDED, bool F32>
 __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkArgs a) {
@@ -653,9 +688,19 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
     n_users = n < n_users ? n : n_users;
     n_ublocks = (n_users + UPWG - 1) / UPWG;
   }
-  const int64_t n_head = a.n_head < n_ublocks ? a.n_head : n_ublocks;
+  int64_t n_head = a.n_head < n_ublocks ? a.n_head : n_ublocks;
+  int tail_chunks = a.tail_chunks;
+  int64_t chunk_items = a.chunk_items, pad_rows = a.n_users_pad;
+  if (a.dev_split > 0) {  // second-tier rescan: every failing block split over the grid
+    const DevSplit ds = dev_split_plan(n_ublocks, gridDim.x, a.dev_split, a.buf_blocks, a.n_items,
+                                       (int64_t)SR * kTileItems);
+    n_head = 0;
+    tail_chunks = ds.chunks;
+    chunk_items = ds.chunk_items;
+    pad_rows = n_ublocks * UPWG;
+  }
   const int64_t n_tail = n_ublocks - n_head;
-  const int64_t n_units = n_head + n_tail * a.tail_chunks;
+  const int64_t n_units = n_head + n_tail * tail_chunks;
   for (int64_t unit = blockIdx.x; unit < n_units; unit += gridDim.x) {
     DG_T0(t_pro);
     int64_t ub, i_beg = 0, i_end = a.n_items, brow;
@@ -667,10 +712,10 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
       const int64_t idx = unit - n_head;
       const int64_t j = idx / n_tail, tb = idx % n_tail;
       ub = n_head + tb;
-      i_beg = j * a.chunk_items;
-      i_end = i_beg + a.chunk_items < a.n_items ? i_beg + a.chunk_items : a.n_items;
-      brow = j == 0 ? ub * UPWG : a.n_users_pad + ((j - 1) * n_tail + tb) * UPWG;
-      chunked = a.tail_chunks > 1;
+      i_beg = j * chunk_items;
+      i_end = i_beg + chunk_items < a.n_items ? i_beg + chunk_items : a.n_items;
+      brow = j == 0 ? ub * UPWG : pad_rows + ((j - 1) * n_tail + tb) * UPWG;
+      chunked = tail_chunks > 1;
     }
     const int ntiles = i_end > i_beg ? (int)((i_end - i_beg + kTileItems - 1) / kTileItems) : 0;
     const int nst = (ntiles + SR - 1) / SR;

@@ -123,7 +123,8 @@ __global__ __launch_bounds__(256) void topk_finalize_kernel(
     int32_t* __restrict__ out_i, const int64_t* __restrict__ pos_map,
     const int32_t* __restrict__ n_users_dev, const int64_t* __restrict__ user_ids,
     int32_t* __restrict__ fail_cnt, int64_t* __restrict__ fail_rows,
-    int64_t* __restrict__ fail_pos) {
+    int64_t* __restrict__ fail_pos, const float* __restrict__ fail_thr_src,
+    float* __restrict__ fail_thr) {
   const int lane = dr::lane_id();
   const int64_t u = u0 + (((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6);
   if (n_users_dev) {
@@ -147,7 +148,118 @@ __global__ __launch_bounds__(256) void topk_finalize_kernel(
   if (fail_cnt && lane == (k - 1) / P && dr::select_key<P>(key, (k - 1) % P) == 0ull) {
     const int32_t f = atomicAdd(fail_cnt, 1);
     fail_rows[f] = user_ids ? user_ids[u] : u;
-    fail_pos[f] = u;
+    fail_pos[f] = op;
+    if (fail_thr) fail_thr[f] = fail_thr_src[u];  // the user's second-tier threshold
+  }
+}
+
+// Drop the keys of excluded items (sorted exclusion list of n items): binary
+// lifting in one uniform loop over the steps, so key[] keeps static indices.
+template <int P>
+__device__ __forceinline__ void drop_excluded(uint64_t (&key)[P], const int32_t* __restrict__ list,
+                                              int n) {
+  if (n <= 0) return;
+  int lo[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) lo[i] = 0;
+  int step = 1;
+  while (2 * step <= n) step *= 2;
+  for (; step > 0; step >>= 1) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int c = lo[i] + step;
+      if (c <= n && list[c - 1] < (int32_t)dr::key_item(key[i])) lo[i] = c;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < P; ++i)
+    if (key[i] != 0ull && lo[i] < n && list[lo[i]] == (int32_t)dr::key_item(key[i])) key[i] = 0ull;
+}
+
+// ------------------------------------------------------------------ second-tier finalize
+// Users of a second-tier rescan (dev_split chunk plan, device count): one
+// wave per user streams the keys of all its chunk buffers, any number of
+// them, through a 2048-key register sort that keeps the running best 1024
+// (elements [0, 1024)); new keys enter elements [1024, 2048). Excluded items
+// are dropped, the k best written to the caller's position pos_map[u]; a user
+// left with fewer than k keys (its second-tier threshold was still too high)
+// goes to the third-tier list.
+struct DevSplitArgs {
+  int upwg, grid, max_c;
+  int64_t buf_blocks, n_items, stage_items;
+};
+
+__global__ __launch_bounds__(256) void topk_finalize_stream_kernel(
+    const uint64_t* __restrict__ cand, const int32_t* __restrict__ cnt, const DevSplitArgs dsa,
+    int cap, int64_t n_users_max, int k, const int64_t* __restrict__ excl_rowptr,
+    const int32_t* __restrict__ excl_items, float* __restrict__ out_s, int32_t* __restrict__ out_i,
+    const int64_t* __restrict__ pos_map, const int32_t* __restrict__ n_users_dev,
+    const int64_t* __restrict__ user_ids, int32_t* __restrict__ fail_cnt,
+    int64_t* __restrict__ fail_rows, int64_t* __restrict__ fail_pos) {
+  constexpr int P = 32;
+  const int lane = dr::lane_id();
+  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  int64_t n = *n_users_dev;
+  n = n < n_users_max ? n : n_users_max;
+  if (u >= n) return;  // wave-uniform
+  const int64_t nb = (n + dsa.upwg - 1) / dsa.upwg;
+  const DevSplit ds = dev_split_plan(nb, dsa.grid, dsa.max_c, dsa.buf_blocks, dsa.n_items,
+                                     dsa.stage_items);
+  const int64_t rows_per_chunk = nb * dsa.upwg;  // chunk j of user u: row j * rows_per_chunk + u
+  int64_t total = 0;
+  for (int j = 0; j < ds.chunks; ++j) total += cnt[j * rows_per_chunk + u];
+  const int64_t op = pos_map[u];
+  const int32_t* ex = nullptr;
+  int exn = 0;
+  if (excl_rowptr) {
+    ex = excl_items + excl_rowptr[op];
+    exn = (int)(excl_rowptr[op + 1] - excl_rowptr[op]);
+  }
+  // keys at flat positions [x0, x0 + 64 * P) of the concatenated buffers into
+  // elements e = lane * P + i with lane >= lane0
+  uint64_t key[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) key[i] = 0ull;
+  auto load = [&](int64_t x0, int lane0) {
+    if (lane < lane0) return;
+    uint64_t nk[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) nk[i] = 0ull;
+    int64_t off = 0;
+    for (int j = 0; j < ds.chunks; ++j) {
+      const int64_t r = j * rows_per_chunk + u;
+      const int64_t nj = cnt[r];
+      const uint64_t* src = cand + (size_t)r * cap;
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const int64_t x = x0 + (int64_t)(lane - lane0) * P + i;
+        if (x >= off && x < off + nj) nk[i] = src[x - off];
+      }
+      off += nj;
+    }
+    drop_excluded<P>(nk, ex, exn);
+#pragma unroll
+    for (int i = 0; i < P; ++i) key[i] = nk[i];
+  };
+  load(0, 0);
+  dr::wave_sort_desc<P>(key);
+  for (int64_t next = 64 * P; next < total; next += 32 * P) {
+    load(next, 32);
+    dr::wave_sort_desc<P>(key);
+  }
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const int e = lane * P + i;
+    if (e < k) {
+      const bool empty = key[i] == 0ull;
+      out_s[op * k + e] = empty ? -INFINITY : dr::key_score(key[i]);
+      out_i[op * k + e] = empty ? -1 : (int32_t)dr::key_item(key[i]);
+    }
+  }
+  if (lane == (k - 1) / P && dr::select_key<P>(key, (k - 1) % P) == 0ull) {
+    const int32_t f = atomicAdd(fail_cnt, 1);
+    fail_rows[f] = user_ids[u];
+    fail_pos[f] = op;
   }
 }
 
@@ -157,31 +269,38 @@ __global__ __launch_bounds__(256) void topk_finalize_kernel(
 // (non-excluded) sample score, so every score >= it passes the scan's
 // `score > thr` test. -inf when the sample holds fewer than k candidates;
 // +inf for padding positions (no user).
+// thr[u] is taken at sample rank k1 (the first tier: the main scan's
+// threshold), thr2[u] at rank k (the safe rank: a second-tier rescan's, for
+// users whose first-tier guess fails); thr2 may be NULL.
 template <int P>
 __global__ __launch_bounds__(256) void topk_threshold_kernel(
     const uint64_t* __restrict__ cand, const int32_t* __restrict__ cnt, const BufMap m, int cap,
-    int64_t u0, int64_t u1, int64_t n_users, int k, float* __restrict__ thr) {
+    int64_t u0, int64_t u1, int64_t n_users, int k, int k1, float* __restrict__ thr,
+    float* __restrict__ thr2) {
   const int lane = dr::lane_id();
   const int64_t u = u0 + (((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6);
   if (u >= u1) return;  // wave-uniform
   if (u >= n_users) {
-    if (lane == 0) thr[u] = INFINITY;
+    if (lane == 0) {
+      thr[u] = INFINITY;
+      if (thr2) thr2[u] = INFINITY;
+    }
     return;
   }
   uint64_t key[P];
   gather_candidates<P>(cand, cnt, m, cap, u, nullptr, nullptr, u, key);
   dr::wave_sort_desc<P>(key);
-  const int e = k - 1;
-  if (lane == e / P) {
-    const uint64_t kk = dr::select_key<P>(key, e % P);
+  auto below_key = [](uint64_t kk) {
     float t = -INFINITY;
     if (kk != 0ull) {
       const float s = dr::key_score(kk);
       const float below = s - fmaxf(fabsf(s) * 0x1p-20f, 0x1p-100f);
       t = below < s ? below : -INFINITY;  // NaN / inf scores: no pruning
     }
-    thr[u] = t;
-  }
+    return t;
+  };
+  if (lane == (k1 - 1) / P) thr[u] = below_key(dr::select_key<P>(key, (k1 - 1) % P));
+  if (thr2 && lane == (k - 1) / P) thr2[u] = below_key(dr::select_key<P>(key, (k - 1) % P));
 }
 
 // ------------------------------------------------------------------ merge
@@ -379,7 +498,8 @@ int tail_keys(const Plan& p, int w, int k) {
 struct Guess {
   int64_t S = 0;       // sample rows (0 = plain scan)
   int64_t stride = 0;  // sample row i is slice row i * stride
-  int ks = 0;          // rank of the guessed threshold in the sample
+  int ks = 0;          // safe rank of the guessed threshold in the sample (second tier)
+  int ks1 = 0;         // first-tier rank (<= ks): the main scan's threshold
 };
 
 #ifndef DR_GUESS
@@ -391,6 +511,15 @@ struct Guess {
 #ifndef DR_GUESS_STRIDE
 #define DR_GUESS_STRIDE 32
 #endif
+// Two-tier guess (round 3): the main scan starts from the sample's
+// ks1-th best score, ks1 = mean + DR_GUESS_TIGHT_Z sigma + 1 (about 0.5-1 %
+// of users fail it); the users it fails are rescanned from their safe
+// (6-sigma) threshold by a second-tier scan spread over every CU, and the
+// rare users that fail that too by the whole-catalog rescan from -inf.
+#ifndef DR_GUESS_TIGHT_Z
+#define DR_GUESS_TIGHT_Z 2.5
+#endif
+constexpr int kMaxRescanChunks = 64;  // catalog chunks per user block of a second-tier rescan
 constexpr int64_t kGuessStride = DR_GUESS_STRIDE;
 constexpr int64_t kGuessMinItems = 1 << 18;
 #ifndef DR_GUESS_MAX_LOG2
@@ -427,6 +556,14 @@ Guess guess_for(int64_t n_items, int k, bool split_tail) {
   const double mu = (double)k * (double)g.S / (double)n_items;
   int ks = (int)ceil(mu + DR_GUESS_SIGMA * sqrt(mu) + 3.0);
   g.ks = ks < k ? ks : k;
+  double z1 = DR_GUESS_TIGHT_Z, c1 = 1.0;
+  if (const char* e = getenv("DIVREC_GUESS_Z1")) z1 = atof(e);  // A/B knobs
+  if (const char* e = getenv("DIVREC_GUESS_C1")) c1 = atof(e);
+  int ks1 = (int)ceil(mu + z1 * sqrt(mu) + c1);
+  if (ks1 < 1) ks1 = 1;
+  const char* tight = getenv("DIVREC_GUESS_TIGHT");  // A/B knob: "0" = one tier (ks1 = ks)
+  if (tight && tight[0] == '0') ks1 = g.ks;
+  g.ks1 = ks1 < g.ks ? ks1 : g.ks;
   return g;
 }
 
@@ -441,18 +578,22 @@ size_t diag_bytes() {
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Workspace layout, 256-B aligned pieces:
-//   [cand | cnt | thr | sample rows | fail rows | fail positions | fail count | diag].
-// The sample scan, the main scan and the rescan run one after the other on
+//   [cand | cnt | thr (tier 1, tier 2) | sample rows | fail rows | fail positions |
+//    fail thresholds | tier-2 fail rows | tier-2 fail positions | fail counts | diag].
+// The sample scan, the main scan and the rescans run one after the other on
 // the stream and share the candidate region.
 struct Layout {
   Plan main, sample;
   Guess g;
-  size_t cand = 0, cnt = 0, thr = 0, samp = 0, frows = 0, fpos = 0, fcnt = 0, diag = 0;
+  size_t cand = 0, cnt = 0, thr = 0, samp = 0, frows = 0, fpos = 0, fthr = 0, fcnt = 0, diag = 0;
   size_t off_thr() const { return cand + cnt; }
-  size_t off_samp() const { return off_thr() + thr; }
+  size_t off_samp() const { return off_thr() + 2 * thr; }
   size_t off_frows() const { return off_samp() + samp; }
   size_t off_fpos() const { return off_frows() + frows; }
-  size_t off_fcnt() const { return off_fpos() + fpos; }
+  size_t off_fthr() const { return off_fpos() + fpos; }
+  size_t off_frows2() const { return off_fthr() + fthr; }
+  size_t off_fpos2() const { return off_frows2() + frows; }
+  size_t off_fcnt() const { return off_fpos2() + fpos; }
   size_t off_diag() const { return off_fcnt() + fcnt; }
   size_t total() const { return off_diag() + diag; }
 };
@@ -474,6 +615,7 @@ Layout make_layout(int64_t n_users, int64_t n_items, int w, int k) {
     L.samp = al256((size_t)L.g.S * w * 2);
     L.frows = al256((size_t)n_users * sizeof(int64_t));
     L.fpos = al256((size_t)n_users * sizeof(int64_t));
+    L.fthr = al256((size_t)n_users * sizeof(float));
     L.fcnt = 256;
   }
   L.diag = diag_bytes();
@@ -578,6 +720,27 @@ extern "C" int dr_score_topk_plan(int64_t n_users, int64_t n_items, int dtype, i
   return DR_OK;
 }
 
+// Users the guessed thresholds failed in the last dr_score_topk call that
+// used this workspace with these arguments: out[0] first tier (rescanned from
+// the safe threshold), out[1] second tier (rescanned from -inf). Host query:
+// a synchronous copy of two device counters (no counters for plain scans: 0).
+extern "C" int dr_score_topk_fail_counts(const void* workspace, int64_t n_users, int64_t n_items,
+                                         int dtype, int d, int k, int32_t* out) {
+  DR_CHECK_ARG(out, "null out");
+  out[0] = out[1] = 0;
+  const int w = width_for(dtype, d);
+  DR_CHECK_ARG(w > 0 && k >= 1 && k <= 1024 && cap_for(w, k) > 0, "unsupported dtype / d / k");
+  DR_CHECK_ARG(workspace && n_users > 0 && n_items > 0, "bad arguments");
+  const Layout L = make_layout(n_users, n_items, w, k);
+  if (L.g.S == 0) return DR_OK;
+  const char* ws = (const char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  DR_CHECK_HIP(hipMemcpy(out, ws + L.off_fcnt(), 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (L.g.ks1 == L.g.ks) {  // one tier: the first count went straight to the -inf rescan
+    out[1] = out[0];
+  }
+  return DR_OK;
+}
+
 #ifdef DR_TOPK_DIAG
 // Diag builds only: byte offset (from the 256-B aligned workspace base) of the
 // [grid*8][16] u64 counter block of the main scan, and its grid size.
@@ -668,7 +831,8 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
 #define DR_FIN(PP)                                                                             \
   hipLaunchKernelGGL((topk_finalize_kernel<PP>), dim3((unsigned)dr::ceil_div(U1 - U0, 4)),      \
                      dim3(256), 0, s, a.cand, a.cnt, FMAP, p.cap, U0, U1, k, excl_rowptr,        \
-                     excl_items, out_scores, out_items, FPOS, FNDEV, user_ids, FCNT, frows, fpos)
+                     excl_items, out_scores, out_items, FPOS, FNDEV, FUIDS, FCNT, frows, fpos,   \
+                     FTSRC, fthr)
   // head users (one buffer each), then the split tail's users (their chunks)
 #define DR_FIN_ALL()                                                        \
   {                                                                         \
@@ -685,20 +849,28 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
     DR_CHECK_LAUNCH();
     int64_t* frows = nullptr;
     int64_t* fpos = nullptr;
+    float* fthr = nullptr;
     const int64_t* FPOS = nullptr;
     const int32_t* FNDEV = nullptr;
+    const int64_t* FUIDS = user_ids;
     int32_t* FCNT = nullptr;
+    const float* FTSRC = nullptr;
     DR_FIN_ALL()
     return DR_OK;
   }
 
   // ---- guessed thresholds: sample scan -> thresholds -> seeded scan -> verify
+  const bool two_tier = L.g.ks1 < L.g.ks;
   float* thr = (float*)(ws + L.off_thr());
+  float* thr2 = two_tier ? (float*)(ws + L.off_thr() + L.thr) : nullptr;
   char* samp = ws + L.off_samp();
   int64_t* frows = (int64_t*)(ws + L.off_frows());
   int64_t* fpos = (int64_t*)(ws + L.off_fpos());
-  int32_t* fcnt = (int32_t*)(ws + L.off_fcnt());
-  DR_CHECK_HIP(hipMemsetAsync(fcnt, 0, sizeof(int32_t), s));
+  float* fthr = two_tier ? (float*)(ws + L.off_fthr()) : nullptr;
+  int64_t* frows2 = (int64_t*)(ws + L.off_frows2());
+  int64_t* fpos2 = (int64_t*)(ws + L.off_fpos2());
+  int32_t* fcnt = (int32_t*)(ws + L.off_fcnt());  // [0] first-tier failures, [1] second-tier
+  DR_CHECK_HIP(hipMemsetAsync(fcnt, 0, 2 * sizeof(int32_t), s));
   {
     const int cpr = w / 8;  // 16-B chunks per row
     const int64_t n16 = L.g.S * cpr;
@@ -727,7 +899,8 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
     const int64_t sh = ps.head_users();
 #define DR_THR(PP)                                                                             \
   hipLaunchKernelGGL((topk_threshold_kernel<PP>), dim3((unsigned)dr::ceil_div(T1 - T0, 4)),     \
-                     dim3(256), 0, s, a.cand, a.cnt, sm, ps.cap, T0, T1, n_users, L.g.ks, thr)
+                     dim3(256), 0, s, a.cand, a.cnt, sm, ps.cap, T0, T1, n_users, L.g.ks,        \
+                     L.g.ks1, thr, thr2)
     int64_t T0 = 0, T1 = sh < p.n_users_pad ? sh : p.n_users_pad;
     if (T1 > T0) { DR_BY_P(p_for(head_keys(ps, w, L.g.ks)), DR_THR) DR_CHECK_LAUNCH(); }
     T0 = T1;
@@ -742,17 +915,58 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   {
     const int64_t* FPOS = nullptr;
     const int32_t* FNDEV = nullptr;
+    const int64_t* FUIDS = user_ids;
     int32_t* FCNT = fcnt;  // verify: users left with fewer than k keys
+    const float* FTSRC = thr2;
     DR_FIN_ALL()
   }
 
-  // ---- rescan of the users whose guess was too high (usually none): whole
-  // catalog units only, one buffer per listed user
+  // ---- second tier (two-tier guesses): the first tier's failures rescanned
+  // from their safe thresholds, every failing user block split over the CUs
+  // (plan on the device: the count is there), any number of keys per user
+  // merged by the streaming finalize; its own failures go to the third tier
+  const int64_t* t3_rows = frows;
+  const int64_t* t3_pos = fpos;
+  const int32_t* t3_cnt = fcnt;
+  if (two_tier) {
+    TopkArgs a2 = a;
+    a2.init_thr = fthr;
+    a2.user_ids = frows;
+    a2.pos_map = fpos;
+    a2.n_users_dev = fcnt;
+    a2.n_head = 0;
+    a2.end_keep = 0;
+    a2.dev_split = kMaxRescanChunks;
+    a2.buf_blocks = p.buf_rows / p.users_per_wg;
+    a2.diag = nullptr;
+    Plan p2 = p;
+    p2.grid = device_cus();
+    DR_SCAN_OR_FAIL(p2, a2, true)
+    DR_CHECK_LAUNCH();
+    DevSplitArgs dsa;
+    dsa.upwg = p.users_per_wg;
+    dsa.grid = p2.grid;
+    dsa.max_c = kMaxRescanChunks;
+    dsa.buf_blocks = a2.buf_blocks;
+    dsa.n_items = n_items;
+    dsa.stage_items = stage_items_for(w);
+    hipLaunchKernelGGL(topk_finalize_stream_kernel, dim3((unsigned)dr::ceil_div(n_users, 4)),
+                       dim3(256), 0, s, a.cand, a.cnt, dsa, p.cap, n_users, k, excl_rowptr,
+                       excl_items, out_scores, out_items, fpos, fcnt, frows, fcnt + 1, frows2,
+                       fpos2);
+    DR_CHECK_LAUNCH();
+    t3_rows = frows2;
+    t3_pos = fpos2;
+    t3_cnt = fcnt + 1;
+  }
+
+  // ---- third tier: the users every guess failed (usually none), rescanned
+  // from -inf; whole-catalog units only, one buffer per listed user
   TopkArgs af = a;
   af.init_thr = nullptr;
-  af.user_ids = frows;
-  af.pos_map = fpos;
-  af.n_users_dev = fcnt;
+  af.user_ids = t3_rows;
+  af.pos_map = t3_pos;
+  af.n_users_dev = t3_cnt;
   af.n_head = p.n_ublocks;
   af.tail_chunks = 1;
   af.chunk_items = n_items;
@@ -763,9 +977,11 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   {
     const BufMap FMAP{p.n_users_pad, p.n_users_pad, 0, 1};
     const int64_t U0 = 0, U1 = n_users;
-    const int64_t* FPOS = fpos;
-    const int32_t* FNDEV = fcnt;
+    const int64_t* FPOS = t3_pos;
+    const int32_t* FNDEV = t3_cnt;
+    const int64_t* FUIDS = t3_rows;
     int32_t* FCNT = nullptr;
+    const float* FTSRC = nullptr;
     DR_BY_P(p_for(head_keys(p, w, k)), DR_FIN)
     DR_CHECK_LAUNCH();
   }
@@ -866,7 +1082,7 @@ extern "C" int dr_score_topk_seeded(const void* user_table, const int64_t* user_
 #define DR_FIN_SEEDED(PP)                                                                       \
   hipLaunchKernelGGL((topk_finalize_kernel<PP>), grid, dim3(256), 0, s, a.cand, a.cnt, bm, p.cap, \
                      U0, U1, k, excl_rowptr, excl_items, out_scores, out_items, nullptr, nullptr,  \
-                     user_ids, nullptr, nullptr, nullptr)
+                     user_ids, nullptr, nullptr, nullptr, nullptr, nullptr)
       switch (P) {
         case 4: DR_FIN_SEEDED(4); break;
         case 8: DR_FIN_SEEDED(8); break;

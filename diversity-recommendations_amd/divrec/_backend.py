@@ -49,6 +49,7 @@ SIGNATURES = {
         [_p, _p, _i64, _p, _i64, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _sz, _p],
     ),
     "dr_score_topk_plan": (_i32, [_i64, _i64, _i32, _i32, _i32, _p, _i32]),
+    "dr_score_topk_fail_counts": (_i32, [_p, _i64, _i64, _i32, _i32, _i32, _p]),
     "dr_score_topk_seeded_workspace": (_sz, [_i64, _i64, _i32, _i32, _i32]),
     "dr_score_topk_seeded": (
         _i32,

@@ -129,6 +129,14 @@ int dr_score_topk(const void* user_table, const int64_t* user_ids, int64_t n_use
 int dr_score_topk_plan(int64_t n_users, int64_t n_items, int dtype, int d, int k, int64_t* out,
                        int n_out);
 
+/* Guess statistics of the last dr_score_topk call on `workspace` with these
+ * arguments (host query; synchronises with a copy): out[0] = users whose
+ * first-tier guessed threshold failed (rescanned from their safe threshold),
+ * out[1] = users every guess failed (rescanned from -inf). 0, 0 for plain
+ * scans (catalogs below 2^18 rows). int32 out[2] is HOST memory. */
+int dr_score_topk_fail_counts(const void* workspace, int64_t n_users, int64_t n_items, int dtype,
+                              int d, int k, int32_t* out);
+
 /* dr_score_topk with caller-given per-user thresholds: the top-k (same order)
  * of the items whose score is STRICTLY above init_thr[u]; slots past the last
  * such item hold item -1 and score -inf. init_thr fp32 [n_users] (-inf = plain

@@ -17,6 +17,9 @@ __all__ = [
     "candidates_for_user",
     "recommend_topk",
     "reference_loop_topk",
+    "reference_mf_forward",
+    "reference_bpr_steps",
+    "mmr_greedy_torch",
     "topk_order",
     "topk_merge",
     "ild_sequential",
@@ -130,6 +133,73 @@ def reference_loop_topk(U, I, k: int, users: Sequence[int], frozen=None):
                                torch.nn.functional.embedding(negatives, I), dim=1)
             recs.append(negatives[torch.argsort(scores, descending=True)][:k].tolist())
     return torch.LongTensor(recs)
+
+
+def reference_mf_forward(U, I, uid, iid):
+    """MatrixFactorization.forward (divrec/models/matrix_factorization.py:26-28)
+    restated in torch for the CPU baseline: two embedding gathers and
+    torch.sum(u * i, dim=1), intra-op parallel on torch's threads like the
+    reference. U, I fp32 torch tables; uid, iid LongTensors."""
+    import torch
+
+    with torch.no_grad():
+        return torch.sum(torch.nn.functional.embedding(uid, U) *
+                         torch.nn.functional.embedding(iid, I), dim=1)
+
+
+def reference_bpr_steps(U, I, batches, lr=1e-3):
+    """pair_wise_train_loop (divrec/train/utils.py:130-164) restated in torch
+    for the CPU baseline: per batch (u, p, n) the reference's two
+    MatrixFactorization forwards, LogSigmoidDifferenceLoss
+    (-logsigmoid(pos - neg), mean; log_sigmoid_difference_loss.py:11-14),
+    backward through dense nn.Embedding gradients and torch.optim.Adam.step
+    + zero_grad over both tables. U, I: fp32 torch tables (trained on
+    copies). Returns (per-batch losses, final U, final I)."""
+    import torch
+
+    ue = torch.nn.Embedding.from_pretrained(U.clone(), freeze=False)
+    ie = torch.nn.Embedding.from_pretrained(I.clone(), freeze=False)
+    opt = torch.optim.Adam(list(ue.parameters()) + list(ie.parameters()), lr=lr)
+    losses = []
+    for uid, pid, nid in batches:
+        pos = torch.sum(ue(uid) * ie(pid), dim=1)
+        neg = torch.sum(ue(uid) * ie(nid), dim=1)
+        per = -torch.nn.functional.logsigmoid(pos - neg)
+        loss = torch.sum(per, 0) / per.size(0)  # ScoreWithReduction 'mean' (base_losses.py:22-27)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        losses.append(float(loss.detach()))
+    return losses, ue.weight.detach(), ie.weight.detach()
+
+
+def mmr_greedy_torch(cand_items, cand_scores, E, k_out, lam):
+    """The build's MMR spec (mmr_greedy) restated as the eager per-user greedy
+    in torch fp32 for the CPU baseline: per user the C x C cosine matrix of
+    the candidates (one GEMM), then k_out argmax rounds over
+    lam * s - (1 - lam) * max_picked cos. cand_items int [n, C], cand_scores
+    fp32 [n, C], E fp32 torch table. Returns LongTensor [n, k_out]."""
+    import torch
+
+    out = []
+    with torch.no_grad():
+        for u in range(cand_items.shape[0]):
+            X = E[cand_items[u].long()]
+            Xn = X / X.norm(dim=1, keepdim=True)
+            S = Xn @ Xn.T
+            s = cand_scores[u]
+            pen = torch.zeros_like(s)
+            alive = torch.ones_like(s, dtype=torch.bool)
+            picks = []
+            for t in range(k_out):
+                val = lam * s - (1 - lam) * pen if t else lam * s
+                val = torch.where(alive, val, torch.full_like(val, -float("inf")))
+                j = int(torch.argmax(val))
+                picks.append(int(cand_items[u, j]))
+                alive[j] = False
+                pen = S[:, j] if t == 0 else torch.maximum(pen, S[:, j])
+            out.append(picks)
+    return torch.LongTensor(out)
 
 
 def topk_merge(scores: np.ndarray, items: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:

@@ -99,6 +99,25 @@ def test_bpr_step():
     assert np.allclose(I1, g["I1"], rtol=0, atol=2e-7)
 
 
+def test_reference_torch_restatements():
+    """The torch restatements bench.py times as CPU baselines reproduce the
+    reference: MatrixFactorization.forward and one pair_wise_train_loop batch
+    (loss, Adam step) bit for bit against the reference-generated fixtures."""
+    import torch
+
+    for d in (32, 64, 128):
+        g = load(f"mf_forward_d{d}")
+        out = oracle.reference_mf_forward(torch.from_numpy(g["U"]), torch.from_numpy(g["I"]),
+                                          torch.from_numpy(g["uid"]), torch.from_numpy(g["iid"]))
+        assert np.array_equal(out.numpy(), g["out"])
+    g = load("bpr_step")
+    losses, U1, I1 = oracle.reference_bpr_steps(
+        torch.from_numpy(g["U0"]), torch.from_numpy(g["I0"]),
+        [(torch.from_numpy(g["uid"]), torch.from_numpy(g["pid"]), torch.from_numpy(g["nid"]))])
+    assert np.float32(losses[0]) == g["loss"]
+    assert np.array_equal(U1.numpy(), g["U1"]) and np.array_equal(I1.numpy(), g["I1"])
+
+
 def test_ml100k_cfg1_recs_and_ild():
     g = load("ml100k_cfg1")
     U, I = g["U"], g["I"]

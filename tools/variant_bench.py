@@ -76,12 +76,12 @@ def main():
     envs = {t: dict(kv.split("=", 1) for kv in t.split("@")[1].split("+")) if "@" in t else {}
             for t in tags}
     stream = torch.cuda.current_stream(dev).cuda_stream
-    outs, times = {}, {t: [] for t in tags}
+    outs, times, fails = {}, {t: [] for t in tags}, {}
 
     def run(t):
         L = libs[t]
         for key in ("DIVREC_SCAN_SPLIT", "DIVREC_SCAN_SEED", "DIVREC_SCAN_SLOTS", "DIVREC_GUESS_STRIDE",
-                    "DIVREC_TAIL_KEYS"):
+                    "DIVREC_TAIL_KEYS", "DIVREC_GUESS_TIGHT", "DIVREC_GUESS_Z1", "DIVREC_GUESS_C1"):
             os.environ.pop(key, None)
         os.environ.update(envs[t])
         dt = () if t.startswith("abi1") else (B.DR_BF16,)
@@ -99,6 +99,12 @@ def main():
         if rc != 0:
             raise RuntimeError(f"{t}: {L.dr_last_error().decode()}")
         torch.cuda.synchronize()
+        if hasattr(L, "dr_score_topk_fail_counts") and not t.startswith("abi1"):
+            fc = (ctypes.c_int32 * 2)()
+            L.dr_score_topk_fail_counts.argtypes = B.SIGNATURES["dr_score_topk_fail_counts"][1]
+            if L.dr_score_topk_fail_counts(ws.data_ptr(), args.users, args.items, *dt, d, args.k,
+                                           ctypes.addressof(fc)) == 0:
+                fails[t] = [int(fc[0]), int(fc[1])]
         return e0.elapsed_time(e1), s, i
 
     for t in tags:  # warm-up + output capture
@@ -120,7 +126,8 @@ def main():
         ok &= same
         med = statistics.median(times[t])
         res["variants"][t] = {"median_ms": med, "min_ms": min(times[t]),
-                              "tflops": flop / (med * 1e-3) / 1e12, "identical": same}
+                              "tflops": flop / (med * 1e-3) / 1e12, "identical": same,
+                              "guess_failures": fails.get(t)}
     print(json.dumps(res), flush=True)
     return 0 if ok else 1
 
