@@ -512,12 +512,12 @@ struct Guess {
 #define DR_GUESS_STRIDE 32
 #endif
 // Two-tier guess (round 3): the main scan starts from the sample's
-// ks1-th best score, ks1 = mean + DR_GUESS_TIGHT_Z sigma + 1 (about 0.5-1 %
+// ks1-th best score, ks1 = mean + DR_GUESS_TIGHT_Z sigma + 1 (about 0.1 %
 // of users fail it); the users it fails are rescanned from their safe
 // (6-sigma) threshold by a second-tier scan spread over every CU, and the
 // rare users that fail that too by the whole-catalog rescan from -inf.
 #ifndef DR_GUESS_TIGHT_Z
-#define DR_GUESS_TIGHT_Z 2.5
+#define DR_GUESS_TIGHT_Z 3.0
 #endif
 constexpr int kMaxRescanChunks = 64;  // catalog chunks per user block of a second-tier rescan
 constexpr int64_t kGuessStride = DR_GUESS_STRIDE;
