@@ -294,7 +294,8 @@ def pmc_traffic(workload: str, config: str, kernel: str, group: int = 0, per_ste
     return total if found else None
 
 
-SCAN_KERNELS = "score_scan_kernel|sample_rows_kernel|topk_threshold_kernel|topk_finalize_kernel"
+SCAN_KERNELS = ("score_scan_kernel|sample_rows_kernel|topk_threshold_kernel|topk_finalize_kernel"
+                "|topk_finalize_stream_kernel")
 N_SIMDS = 256 * 4  # MI355X: 256 CUs x 4 SIMDs
 
 

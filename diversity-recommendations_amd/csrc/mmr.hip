@@ -675,12 +675,13 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
     auto cidx = [&](int j) { return w * 128 + 32 * j + q; };
     MG_T0(t_sel);
 
-    // ---- probes: the kPPW best live candidates of this wave + its bound, by
-    // the key order (value desc, position asc). Lane (q, h) ranks tiles 2h and
-    // 2h+1 (both half-waves hold the same candidates; this way each counts
-    // once) by the 32-bit value order ord(v) (0 = not live): one wave max per
-    // step; the candidate's position follows from its lane and tile, so the
-    // 64-bit key is needed only when two candidates tie on the value.
+    // ---- probes of this wave and its bound. Any probe set is exact as long
+    // as the bound is the best key outside it, so the wave takes every live
+    // candidate whose value beats the 9th-best value p of its 128 (at most
+    // kPPW of them), found by a radix select over the 32-bit value order:
+    // one ballot pair per bit, no serial argmax chain. The bound is (p, the
+    // lowest position holding p). Lane (q, h) ranks tiles 2h and 2h+1 (both
+    // half-waves hold the same candidates; this way each counts once).
     uint32_t v2[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -695,49 +696,42 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
       }
       v2[i] = o;
     }
+    uint32_t p9 = 0u;  // largest p with at least kPPW + 1 values >= p (0: fewer live)
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t c = p9 | (1u << bit);
+      const int n = __popcll(__ballot(v2[0] >= c)) + __popcll(__ballot(v2[1] >= c));
+      p9 = n >= kPPW + 1 ? c : p9;
+    }
+    const uint64_t b0 = __ballot(v2[0] > p9), b1 = __ballot(v2[1] > p9);
+    const int n0 = __popcll(b0), nprobe = n0 + __popcll(b1);
     uint32_t myslot = 0u;  // per tile j: probe slot + 1 of this lane's candidate (bits 8j..)
 #pragma unroll
-    for (int m = 0; m <= kPPW; ++m) {
-      const uint32_t mh = wmax_u32<64>(v2[0] > v2[1] ? v2[0] : v2[1]);
-      uint64_t best = 0ull;  // key of the m-th best candidate (0 = none)
-      int bl = -1, bi = 0;   // its lane and register (0: tile 2h, 1: tile 2h+1)
-      if (mh != 0u) {
-        const uint64_t b0 = __ballot(v2[0] == mh), b1 = __ballot(v2[1] == mh);
-        if (__popcll(b0) + __popcll(b1) == 1) {
-          bi = b0 ? 0 : 1;
-          bl = __builtin_ctzll(b0 | b1);
-        } else {  // equal values: lowest position wins (exact 64-bit keys)
-          uint64_t lk = 0ull;
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int pos = kWaves * (32 * (2 * h + i) + q) + w;
-            const uint64_t key = v2[i] == mh ? ((uint64_t)mh << 32) | (uint32_t)~pos : 0ull;
-            lk = dr::umax64(lk, key);
-          }
-          const uint64_t kb = wave_max_u64(lk);
-          const int pos = (int)dr::key_item(kb);
-          const int pq = (pos >> 3) & 31, pj = (pos >> 3) >> 5;
-          bl = pq + 32 * (pj >> 1);
-          bi = pj & 1;
-        }
-        const int pj = 2 * (bl >> 5) + bi;
-        const int pos = kWaves * (32 * pj + (bl & 31)) + w;
-        best = ((uint64_t)mh << 32) | (uint32_t)~pos;
+    for (int i = 0; i < 2; ++i) {
+      const uint64_t bm = i == 0 ? b0 : b1;
+      if ((bm >> lane) & 1ull) {
+        const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0));
+        const int slot = w * kPPW + (i == 0 ? 0 : n0) + rank;
+        const int j = 2 * h + i;
+        s_pcand[slot] = kWaves * (32 * j + q) + w;
+        myslot |= (uint32_t)(slot + 1) << (8 * j);
       }
-      if (m == kPPW) {
-        if (lane == 0) s_wbound[w] = best;
-        break;
-      }
-      const int slot = w * kPPW + m;
-      int pc = -1;
-      if (best != 0ull) {
-        pc = (int)dr::key_item(best);
-        if (lane == bl) v2[bi] = 0u;
-        const int pj = (pc >> 3) >> 5, pq = (pc >> 3) & 31;
-        if (q == pq) myslot |= (uint32_t)(slot + 1) << (8 * pj);
-      }
-      if (lane == 0) s_pcand[slot] = pc;
     }
+    myslot |= (uint32_t)__shfl_xor((int)myslot, 32);  // the other half-wave holds the same rows
+    if (lane < kPPW && lane >= nprobe) s_pcand[w * kPPW + lane] = -1;
+    uint64_t wb = 0ull;  // the wave's bound: value p9 at its lowest position among the rest
+    if (p9 != 0u) {
+      uint32_t mp = 0xffffffffu;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        if (v2[i] == p9) {
+          const uint32_t pos = (uint32_t)(kWaves * (32 * (2 * h + i) + q) + w);
+          mp = pos < mp ? pos : mp;
+        }
+      mp = wave_min_u32_64(mp);
+      wb = ((uint64_t)p9 << 32) | (uint32_t)~mp;
+    }
+    if (lane == 0) s_wbound[w] = wb;
     MG_ADD(kMgSelect, t_sel);
     MG_T0(t_stage);
 #pragma unroll

@@ -131,6 +131,7 @@ def score_topk(
     item_base: int = 0,
     exclude: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
     init_thr: Optional[torch.Tensor] = None,
+    stats: Optional[dict] = None,
 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Top-k items per user over the catalog slice ``item_table`` (global ids
     ``item_base + row``); order = score desc, item id asc.
@@ -151,6 +152,10 @@ def score_topk(
     (default: all) are scored. ``exclude = (rowptr int64 [n+1], items int32)``
     is a CSR of GLOBAL item ids (sorted per row) never to recommend.
     Returns (scores fp32 [n, k], items int32 [n, k]).
+
+    ``stats`` (a dict, optional): filled with ``guess_failures`` = [users the
+    first-tier guessed threshold failed, users every guess failed] of this
+    call (dr_score_topk_fail_counts; one synchronising read).
     """
     dev = B.require_device(user_table, item_table, user_ids)
     _need(user_table.dtype == item_table.dtype and user_table.dtype in SCORE_WIDTHS,
@@ -212,6 +217,14 @@ def score_topk(
         ws.data_ptr(), ws.numel(), B.stream(dev),
     )
     B.check(rc, "dr_score_topk")
+    if stats is not None:
+        import ctypes
+
+        torch.cuda.synchronize(dev)
+        fc = (ctypes.c_int32 * 2)()
+        B.check(L.dr_score_topk_fail_counts(ws.data_ptr(), n, n_items, dt, w, int(k),
+                                            ctypes.addressof(fc)), "dr_score_topk_fail_counts")
+        stats["guess_failures"] = [int(fc[0]), int(fc[1])]
     return scores, items
 
 

@@ -157,6 +157,58 @@ def test_forced_stride_k1000_split():
     _check(Ub, Ib, it, s, rows, k)
 
 
+@pytest.mark.parametrize("d,k,nu", [(64, 100, 2 * 2048 + 700), (128, 1000, 3 * 1024 + 55),
+                                    (128, 100, 5 * 1024 + 1)])
+def test_second_tier_every_user_exact(d, k, nu):
+    """The two-tier guess with the first tier forced almost useless
+    (DIVREC_GUESS_Z1=-5: the main scan starts from the sample's best score or
+    so): nearly every user fails the first tier and is recomputed by the
+    second tier, whose device-side plan splits the many failing blocks over
+    the grid and whose streaming finalize merges any number of keys per user
+    (k = 1000: more than one 2048-key round). Exclusions of some users' best
+    items; lists exact; the failure counts show who took which tier."""
+    rng = np.random.default_rng(d + k + nu)
+    ni = (1 << 18) + 5
+    U = rng.integers(-3, 4, size=(nu, d)).astype(np.float32)
+    I = rng.integers(-3, 4, size=(ni, d)).astype(np.float32)
+    frozen = [rng.choice(ni, size=int(rng.integers(0, 20)), replace=False) for _ in range(nu)]
+    for n in range(0, nu, 71):
+        frozen[n] = np.union1d(frozen[n], np.argsort(-(I @ U[n]), kind="stable")[:12])
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    Ub, Ib = torch.from_numpy(U).to(DEV).to(torch.bfloat16), torch.from_numpy(I).to(DEV).to(torch.bfloat16)
+    st = {}
+    with _Env(DIVREC_GUESS_Z1=-5):
+        s, it = ops.score_topk(Ub, Ib, k, exclude=(torch.from_numpy(rowptr).to(DEV),
+                                                   torch.from_numpy(cols).to(DEV)), stats=st)
+    t1, t2 = st["guess_failures"]
+    assert t1 >= 0.9 * nu and t2 <= t1 // 10, st
+    rows = np.unique(np.concatenate([np.arange(0, nu, 7), [nu - 1]]))
+    _check(Ub, Ib, it, s, rows, k, frozen=frozen)
+
+
+def test_second_tier_hot_rows_exact():
+    """8 hot rows at stride-32 sample positions are the best items of a
+    non-negative user group: the first-tier rank in the sample (ks1 = 7 for
+    k = 50) is below 8, so the group fails the first tier; the safe rank
+    (13) reaches 5 normal sample items past the hot rows, so the second tier
+    succeeds for nearly all of them (a user with 5 of its top ~42 normal
+    items in the sample, ~1 %, takes the -inf rescan). Lists exact."""
+    rng = np.random.default_rng(1010)
+    d, ni, k, nu = 64, (1 << 18) + 31, 50, 2 * 2048 + 99
+    plan = ops.score_topk_plan(nu, ni, torch.bfloat16, d, k)
+    assert plan["sample_stride"] == 32
+    U = np.concatenate([rng.integers(0, 4, size=(nu // 2, d)),
+                        rng.integers(-3, 4, size=(nu - nu // 2, d))]).astype(np.float32)
+    I = rng.integers(-3, 4, size=(ni, d)).astype(np.float32)
+    I[np.arange(8) * 32] = 3.0
+    Ub, Ib = torch.from_numpy(U).to(DEV).to(torch.bfloat16), torch.from_numpy(I).to(DEV).to(torch.bfloat16)
+    st = {}
+    s, it = ops.score_topk(Ub, Ib, k, stats=st)
+    t1, t2 = st["guess_failures"]
+    assert t1 >= nu // 2 and t2 <= t1 // 10, st
+    _check(Ub, Ib, it, s, np.arange(0, nu, 3), k)
+
+
 # --------------------------------------------------------------------------- full size
 def _sample_rows(rng, plan, n_users, n_head, n_tail, n_last):
     """Positions from head blocks, from split-tail blocks and from the last
