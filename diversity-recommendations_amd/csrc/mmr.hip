@@ -683,18 +683,25 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
     // lowest position holding p). Lane (q, h) ranks tiles 2h and 2h+1 (both
     // half-waves hold the same candidates; this way each counts once).
     uint32_t v2[2];
+    float r_sc[2], r_pen[2];  // the ranked candidates' score and max term (probe state)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const float sc = s_cscore[w * 128 + 32 * (2 * h + i) + q];
       uint32_t o = 0u;
+      float pn = 0.f;
 #pragma unroll
       for (int j = 0; j < kTiles; ++j) {
-        if (j == 2 * h + i && ((live >> j) & 1u)) {
-          const float val = t == 0 ? lambda * sc : fmaf(-mu, pen[j], lambda * sc);
-          o = dr::f32_to_ord(val);
+        if (j == 2 * h + i) {
+          pn = pen[j];
+          if ((live >> j) & 1u) {
+            const float val = t == 0 ? lambda * sc : fmaf(-mu, pen[j], lambda * sc);
+            o = dr::f32_to_ord(val);
+          }
         }
       }
       v2[i] = o;
+      r_sc[i] = sc;
+      r_pen[i] = pn;
     }
     uint32_t p9 = 0u;  // largest p with at least kPPW + 1 values >= p (0: fewer live)
     for (int bit = 31; bit >= 0; --bit) {
@@ -713,7 +720,14 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0));
         const int slot = w * kPPW + (i == 0 ? 0 : n0) + rank;
         const int j = 2 * h + i;
-        s_pcand[slot] = kWaves * (32 * j + q) + w;
+        const int pos = kWaves * (32 * j + q) + w;
+        // the probe's state, written by the lane that ranked it (its row is
+        // staged below by the two lanes that hold its halves)
+        s_pcand[slot] = pos;
+        s_pitem[slot] = s_citem[pos];
+        s_pinv[slot] = s_cinv[w * 128 + 32 * j + q];
+        s_pscore[slot] = r_sc[i];
+        s_ppen[slot] = r_pen[i];
         myslot |= (uint32_t)(slot + 1) << (8 * j);
       }
     }
@@ -741,12 +755,6 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
 #pragma unroll
         for (int s = 0; s < KS; ++s)
           s_prow[sl * CPR + ((2 * s + h) ^ (sl & SWM))] = __builtin_bit_cast(uint4, brow[j][s]);
-        if (h == 0) {
-          s_pitem[sl] = s_citem[cpos(j)];
-          s_pinv[sl] = s_cinv[cidx(j)];
-          s_pscore[sl] = s_cscore[cidx(j)];
-          s_ppen[sl] = pen[j];
-        }
       }
     }
     MG_T0(t_sbar);

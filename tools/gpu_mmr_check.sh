@@ -4,4 +4,3 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 timeout -k 10 300 python tools/mmr_diag.py --users 65536 --real > gpurun_out/mmr4/diag_real.json 2> gpurun_out/mmr4/diag_real.err
 timeout -k 10 300 python tools/mmr_ab.py --libs product,mmrlegacy --users 262144 --real > gpurun_out/mmr4/ab_real.json 2> gpurun_out/mmr4/ab_real.err
 timeout -k 10 300 python tools/mmr_ab.py --libs product,mmrlegacy --users 262144 > gpurun_out/mmr4/ab_rand.json 2> gpurun_out/mmr4/ab_rand.err
-timeout -k 10 400 python -u -m pytest tests/test_real_plans.py -m gpu -x -v --timeout 300 --timeout-method thread -k "second_tier" > gpurun_out/mmr4/tier2_tests.log 2>&1
