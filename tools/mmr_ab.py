@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--users", type=int, default=262144)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--lam", type=float, default=0.5)
+    ap.add_argument("--check", type=int, default=64,
+                    help="users per variant whose lists differ from the first tag to replay in float64")
     ap.add_argument("--real", action="store_true",
                     help="candidates = the real top-C lists of random users (dr_score_topk)")
     args = ap.parse_args()
@@ -69,7 +71,31 @@ def main():
         res["variants"][t] = {"median_ms": med, "users_per_s": args.users / med * 1e3,
                               "identical": bool(torch.equal(outs[t], outs[tags[0]])),
                               "users_differ": int((outs[t] != outs[tags[0]]).any(dim=1).sum())}
+        if t != tags[0] and args.check:
+            res["variants"][t]["divergence"] = divergence(outs[tags[0]], outs[t], cand.cpu(), sc.cpu(),
+                                                          items, args.lam, args.check)
     print(json.dumps(res), flush=True)
+
+
+def divergence(a, b, cand, sc, items, lam, limit):
+    """Where two variants' lists differ: the float64 MMR values of both choices
+    at the first differing step (the common prefix is the selected set). A gap
+    of a few fp32 ulps means an fp32 near-tie that the two cosine roundings
+    order differently; both lists are then the exact greedy on their values."""
+    rows = torch.nonzero((a != b).any(dim=1)).flatten()[:limit].tolist()
+    worst_gap, worst_rel = 0.0, 0.0
+    for u in rows:
+        p = int(torch.nonzero(a[u] != b[u])[0])
+        pos = {int(x): j for j, x in enumerate(cand[u].tolist())}
+        S = [pos[int(x)] for x in a[u, :p].tolist()]
+        E = items[cand[u].long().clamp(min=0)].double().cpu()
+        E = E / E.norm(dim=1, keepdim=True)
+        pen = (E @ E[S].T).max(dim=1).values if S else torch.zeros(len(E), dtype=torch.float64)
+        val = lam * sc[u].double() - (1 - lam) * (pen if S else 0 * pen)
+        va, vb = float(val[pos[int(a[u, p])]]), float(val[pos[int(b[u, p])]])
+        worst_gap = max(worst_gap, abs(va - vb))
+        worst_rel = max(worst_rel, abs(va - vb) / max(abs(va), 1e-30))
+    return {"checked": len(rows), "max_abs_gap": worst_gap, "max_rel_gap": worst_rel}
 
 
 if __name__ == "__main__":
