@@ -527,7 +527,7 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
   __shared__ int s_citem[kMaxC];
   __shared__ float s_cscore[kMaxC], s_cinv[kMaxC];  // wave-local index cidx
   __shared__ uint64_t s_wbound[kWaves];
-  __shared__ int s_state[4];  // rounds done, picks this batch, picked mask lo / hi
+  __shared__ int s_state[5];  // rounds done, picks this batch, picked mask lo / hi, forced pick
   __shared__ int s_out[kMaxC];
   auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
@@ -825,7 +825,8 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
       const uint32_t bhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bound >> 32));
       const uint32_t blo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bound);
       // t >= 1 here whenever a live candidate exists (the first pick is made
-      // before the batches), so every live max term is finite
+      // before the batches: values only fall from then on, which the bound
+      // needs), so every live max term is finite
       bool alive = pa >= 0;
       uint32_t cur = alive ? ordv(fmaf(-mu, pna, lsa)) : 0u;
       int rec_slot = -1;  // lane i: probe slot of pick i of this batch
@@ -864,11 +865,16 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
         for (int i = t + lane; i < k_out; i += 64) s_out[i] = -1;
         t = k_out;
       }
+      // No probe beats the bound (>= kPPW + 1 equal values at the top of
+      // every wave that has one): the bound's candidate, the best key outside
+      // the probes, is the next pick.
+      const int forced = (np == 0 && t < k_out && (bhi | blo) != 0u) ? (int)~blo : -1;
       if (lane == 0) {
         s_state[0] = t;
         s_state[1] = np;
         s_state[2] = (int)(uint32_t)picked;
         s_state[3] = (int)(uint32_t)(picked >> 32);
+        s_state[4] = forced;
       }
     }
     MG_ADD(kMgRounds, t_rounds);
@@ -877,17 +883,43 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
     t = s_state[0];
     const int np = s_state[1];
     const uint64_t picked = (uint64_t)(uint32_t)s_state[2] | ((uint64_t)(uint32_t)s_state[3] << 32);
+    const int forced = s_state[4];
     MG_ADD(kMgSync2, t_sync2);
     MG_T0(t_fold);
 
-    // ---- fold: the picks (rows of A, in pick order, 32 per pass) against
-    // every candidate
-    fold(np, h, q);
-    // picked probes of this wave leave the live set
+    if (t >= k_out) break;  // the list is full: no fold, no further batch
+    if (forced >= 0) {
+      // the forced pick: its owner lanes stage its row as pick 0, then one fold
+      const int fj = (forced >> 3) >> 5, fq = (forced >> 3) & 31;
+      if (w == (forced & 7) && q == fq) {
 #pragma unroll
-    for (int j = 0; j < kTiles; ++j) {
-      const int sl = (int)((myslot >> (8 * j)) & 255u) - 1;
-      if (sl >= 0 && ((picked >> sl) & 1ull)) live &= ~(1u << j);
+        for (int j = 0; j < kTiles; ++j) {
+          if (j == fj) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s) s_prow[2 * s + h] = __builtin_bit_cast(uint4, brow[j][s]);
+          }
+        }
+        if (h == 0) {
+          s_plist[0] = 0;
+          s_lpinv[0] = s_cinv[w * 128 + 32 * fj + q];
+          s_out[t] = s_citem[forced];
+        }
+        live &= ~(1u << fj);
+      }
+      t += 1;
+      lds_barrier();
+      if (t >= k_out) break;
+      fold(1, h, q);
+    } else {
+      // ---- fold: the picks (rows of A, in pick order, 32 per pass) against
+      // every candidate
+      fold(np, h, q);
+      // picked probes of this wave leave the live set
+#pragma unroll
+      for (int j = 0; j < kTiles; ++j) {
+        const int sl = (int)((myslot >> (8 * j)) & 255u) - 1;
+        if (sl >= 0 && ((picked >> sl) & 1ull)) live &= ~(1u << j);
+      }
     }
     lds_barrier();  // LDS probe state is rewritten by the next batch
     MG_ADD(kMgFold, t_fold);

@@ -377,6 +377,9 @@ int cap_for(int w, int k) {
 }
 
 constexpr int kMaxTailChunks = 16;
+#ifndef DR_LONG_FLUSH
+#define DR_LONG_FLUSH 1  // 0: long lists flush at k + kSlack + kFlushGap (A/B only)
+#endif
 // Compaction slack and flush gap of the sample scan (ks <= ~70 keys per user).
 #ifndef DR_SAMPLE_SLACK
 #define DR_SAMPLE_SLACK 32
@@ -448,7 +451,14 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   p.chunk_items = best_c > 1
       ? dr::ceil_div(dr::ceil_div(n_items, best_c), stage_items) * stage_items : n_items;
   p.slack = kSlack;
-  p.gap = kFlushGap;
+  // Long lists: once k + kSlack + kFlushGap passes 1024 keys the head finalize
+  // sorts 2048 keys anyway, so a buffer may fill to CAP - margin before its
+  // first compaction at no finalize cost. A seeded k = 1000 scan admits ~1.5 k
+  // survivors (the guess's rank): with the flush at k + 128 = 1128 every user
+  // compacted a ~1.1K-key buffer 3-4 times in the last third of the catalog;
+  // at CAP - margin = 1792 most users never compact.
+  p.gap = head_flush > kMaxTailKeys && DR_LONG_FLUSH ? p.cap - (int)stage_items - k - kSlack
+                                                     : kFlushGap;
   // a tail chunk ends with at most end_keep >= k keys, so c of them fit the
   // finalize's max_keys
   p.end_keep = best_c > 1 ? std::min(k + kSlack, max_keys / best_c) : 0;

@@ -799,6 +799,30 @@ def test_mmr_rerank_config5_shape(d, C, kout, lam):
         assert np.array_equal(got, cand[:, :kout])
 
 
+@pytest.mark.parametrize("lam", [1.0, 0.5])
+def test_mmr_rerank_ties(lam):
+    """Tie-saturated lists: equal scores everywhere (user 0, 1) and 100 items
+    repeated 10 times with equal scores per item (users 2, 3). More than a
+    wave's probe count of equal values sit at the top of every wave, so a batch
+    can have no probe that beats its bound: the bound's candidate (the best key
+    outside the probes) is then picked on its own. lam = 1 with equal scores
+    must return the candidates in position order (ties: lowest position)."""
+    rng = np.random.default_rng(21)
+    d, ni, C, kout = 128, 5000, 1000, 100
+    E = oracle.as_bf16_f32((rng.standard_normal((ni, d)) / np.sqrt(d)).astype(np.float32))
+    cand = np.stack([rng.choice(ni, C, replace=False) for _ in range(2)]
+                    + [np.repeat(rng.choice(ni, C // 10, replace=False), 10) for _ in range(2)]
+                    ).astype(np.int32)
+    sc = np.full(cand.shape, 0.25, np.float32)
+    sc[2:] = np.repeat(-np.sort(-rng.random((2, C // 10))), 10, axis=1)
+    got = ops.mmr_rerank(torch.from_numpy(cand).to(DEV), torch.from_numpy(sc).to(DEV), _bf16(E),
+                         kout, lam).cpu().numpy()
+    assert _mmr_check_positions(got, cand, sc, E, lam, tol=1e-4) == 0
+    if lam == 1.0:
+        assert np.array_equal(got[:2], cand[:2, :kout])
+        assert np.array_equal(got[2:], cand[2:, :kout])
+
+
 def test_mmr_rerank_invalid_candidates():
     """-1 candidates are never picked; once the live ones run out the tail is -1."""
     rng = np.random.default_rng(5)

@@ -1,0 +1,6 @@
+set -e
+mkdir -p gpurun_out/mmr7
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "mmr" > gpurun_out/mmr7/tests.log 2>&1
+timeout -k 10 300 python tools/mmr_ab.py --libs product,mmrprev --users 262144 --real > gpurun_out/mmr7/ab_real.json 2> gpurun_out/mmr7/ab_real.err
+timeout -k 10 300 python tools/mmr_ab.py --libs product,mmrprev --users 262144 > gpurun_out/mmr7/ab_rand.json 2> gpurun_out/mmr7/ab_rand.err
+timeout -k 10 300 python tools/mmr_diag.py --users 65536 --real > gpurun_out/mmr7/diag_real.json 2> gpurun_out/mmr7/diag_real.err
