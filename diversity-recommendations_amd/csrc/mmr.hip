@@ -4,39 +4,32 @@
 //   pick_t = argmax_{i not picked} lambda * s_i - (1 - lambda) * max_{j picked} cos(e_i, e_j)
 // (the max term is 0 before the first pick; ties -> lowest candidate position).
 //
-// Probe-batch design. One 512-thread workgroup per user:
-//   * The C <= 1024 candidate rows stay in registers as MFMA B fragments for
-//     the whole user (wave w owns positions w, w+8, ..., 4 tiles of 32).
-//   * A batch picks 32 PROBES: the 4 best live candidates of every wave by the
-//     current MMR value, and records BOUND = the best value outside them.
-//     One v_mfma_f32_32x32x16_bf16 pass gives the cosine of every candidate
-//     with every probe (probe rows staged in LDS): 32 columns of the greedy's
-//     similarity matrix for the price of 2 VALU rounds of the eager method.
-//   * Fast rounds: the greedy runs over the probes only (their pairwise
-//     cosines sit in LDS), on one wave: a pick is the argmax of the probes'
-//     values, valid while it beats BOUND. Values only fall once a pick exists
-//     (the max term grows), so no non-probe can overtake a probe that beats
-//     BOUND: the picks are exactly the eager greedy's. No barrier per round.
-//   * When a probe no longer beats BOUND (or after round 0, whose max term is
-//     0), the batch ends: every candidate folds the batch's picked columns into
-//     its max term and a new batch starts. ~9.6 batches for 100 picks of 1000
-//     random candidates (lambda = 0.5), ~12.6 on real top-1000 lists.
-// The kernel below is the round-2 layout of this design (mmr_batch_kernel).
+// Probe-batch design, one 512-thread workgroup per CU
+// looping over users (persistent grid):
+//   * A user's C <= 1024 candidate rows stay in registers as MFMA B fragments
+//     (wave w owns positions w, w+8, ..., 4 tiles of 32): half the register
+//     file, so a CU holds one user; the next user's ids, scores and tile-0
+//     rows arrive by LDS-DMA while this one runs.
+//   * A batch takes 64 PROBES (the 8 best live candidates of every wave by
+//     the current MMR value) and BOUND, the best key outside them.
+//   * Fast rounds run the greedy over the probes only, on one wave, with the
+//     probes' 64 x 64 Gram: a pick is valid while it beats BOUND. Values only
+//     fall once a pick exists (the max term grows), so no non-probe can
+//     overtake a probe that beats BOUND: the picks are exactly the eager
+//     greedy's.
+//   * When no probe beats BOUND the batch ends: one MFMA pass of the batch's
+//     picks against every candidate folds their cosines into the max terms.
 #include "common.h"
 
 namespace {
 
-#ifndef DR_MMR_ALLWAVES
-#define DR_MMR_ALLWAVES 0  // fast rounds on every wave instead of wave 0 + a barrier (A/B knob)
-#endif
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
 constexpr int kTiles = 4;                          // candidate tiles of 32 per wave
 constexpr int kMaxC = kWaves * kTiles * 32;        // 1024
-constexpr int kProbes = 32;                        // one MFMA M dimension
-constexpr int kPerWave = kProbes / kWaves;         // probes chosen by each wave
 
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 using dr::bf16x8;
 using dr::f32x16;
 
@@ -50,23 +43,6 @@ __device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
   const int nlo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW_MASK, 0xF, false);
   const int nhi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW_MASK, 0xF, false);
   return ((uint64_t)(uint32_t)nhi << 32) | (uint32_t)nlo;
-}
-// Max / min over lanes 0..31 (rows 0 and 1), result read from lane 31.
-__device__ __forceinline__ uint32_t wave_max_u32_32(uint32_t v) {
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xA, 0xF, false));
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
-}
-__device__ __forceinline__ uint32_t wave_min_u32_32(uint32_t v) {
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xA, 0xF, false));
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
 }
 __device__ __forceinline__ uint32_t wave_min_u32_64(uint32_t v) {
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
@@ -108,26 +84,6 @@ __device__ unsigned long long g_mmr_diag[kWaves][16];
 enum { kMgLoad, kMgSelect, kMgStage, kMgMma, kMgSync1, kMgRounds, kMgSync2, kMgFold, kMgBatches,
        kMgTotal, kMgStageBar, kMgGt, kMgSlots = 16 };
 
-// Max of a float over the wave's 64 lanes by fused v_max_f32_dpp steps (one
-// VALU each), read from lane 63. -inf is the identity (bound_ctrl lanes read 0
-// and are masked by the row masks of the broadcast steps only, so the input
-// of every lane takes part; no NaN reaches here).
-__device__ __forceinline__ float wmax_f32(float v) {
-  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false)));
-  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false)));
-  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false)));
-  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false)));
-  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0x142, 0xA, 0xF, false)));
-  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                   __builtin_bit_cast(int, v), __builtin_bit_cast(int, v), 0x143, 0xC, 0xF, false)));
-  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
-}
-
 // Max over the wave's 64 lanes (lanes = 64) or over lanes 0..31 (lanes = 32)
 // by fused v_max_u32_dpp steps (one VALU each: the reduction is the latency
 // of the serial chains below); the result is read from the last lane.
@@ -145,346 +101,6 @@ __device__ __forceinline__ uint32_t wmax_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
   }
 }
-
-// Round-2 layout of the probe-batch kernel: the same probes, bound and exact
-// fast rounds as mmr_probe_kernel (identical picks), rebuilt around latency:
-//   * the batch's 32 similarity columns stay where the MFMAs leave them
-//     (4 accumulators = 64 VGPRs per lane) instead of 128 KB of LDS; the fold
-//     reads the picked columns there (constant register pattern per lane
-//     half, one v_permlane32_swap per tile);
-//   * probe selection ranks by the 32-bit value order (fused-DPP max, one
-//     VALU per step), falling back to the exact 64-bit (value, position) key
-//     only when two lanes tie on the value; the winner's owners stage its row
-//     at once (the winner's tile and lane are uniform), so no probe-slot map
-//     is read back from LDS;
-//   * per-candidate score, 1/|e| and id live in LDS (registers hold the rows
-//     and the columns).
-// Out-of-range ids (>= n_items) are counted in *err and never picked.
-#ifndef DR_MMR_LEGACY
-#define DR_MMR_LEGACY 0  // 1: the round-2 kernel below (A/B of the round-3 rewrite only)
-#endif
-#if DR_MMR_LEGACY
-template <int D>
-__global__ __launch_bounds__(kThreads) void mmr_batch_kernel(
-    const int32_t* __restrict__ cand_items, const float* __restrict__ cand_scores, int C,
-    const __bf16* __restrict__ E, int64_t n_items, int k_out, float lambda,
-    int32_t* __restrict__ out_items, int32_t* __restrict__ err) {
-  constexpr int KS = D / 16;  // MFMA k-steps per row
-  constexpr int CPR = D / 8;  // 16-B chunks per row
-  constexpr int SWM = (CPR < 16 ? CPR : 16) - 1;
-  constexpr int GTS = 36;  // s_gt row stride in floats: 16-B rows, conflict-free row reads
-  __shared__ uint4 s_prow[kProbes * CPR];  // probe rows, chunk c of row p at p*CPR + (c ^ (p & SWM))
-  // s_gt[a*GTS + p] = cos(probe a, probe p) as candidate a's accumulator holds
-  // it (the same rounding the fold applies to a's max term)
-  __shared__ __attribute__((aligned(16))) float s_gt[kProbes * GTS];
-  __shared__ float s_pinv[kProbes], s_pscore[kProbes], s_ppen[kProbes];
-  __shared__ int s_pcand[kProbes];  // candidate position of each probe slot (-1 = empty)
-  __shared__ int s_pitem[kProbes];  // its item id
-  __shared__ int s_citem[kMaxC];    // candidate position -> item id
-  // per-candidate score and 1/|e|, indexed wave-locally: position c at
-  // cidx(c) = (c & 7) * 128 + (c >> 3), i.e. wave w, tile j, lane q at w*128 + 32j + q
-  __shared__ float s_cscore[kMaxC], s_cinv[kMaxC];
-  __shared__ uint64_t s_wbound[kWaves];
-  __shared__ int s_round[2];  // rounds done, picked probe mask (written by wave 0)
-  __shared__ int s_out[kMaxC];
-  // the picks, stored to HBM once at the end
-  // Barriers inside the batch loop order LDS only: a raw s_barrier after
-  // lgkmcnt(0), so no wave waits there for its outstanding global stores.
-  auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-
-  const int64_t u = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, q = lane & 31;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave index in an SGPR
-  const float mu = 1.f - lambda;
-  auto cpos = [&](int j) { return kWaves * (32 * j + q) + w; };  // this lane's position in tile j
-  auto cidx = [&](int j) { return w * 128 + 32 * j + q; };      // = (cpos & 7) * 128 + (cpos >> 3)
-#ifdef DR_MMR_DIAG
-  uint64_t dg[kMgSlots] = {};
-#endif
-  MG_T0(t_kernel);
-
-  // ---- candidate rows -> B fragments (lane: position cpos(j), k = 16s + 8h .. +7)
-  bf16x8 brow[kTiles][KS];
-  float pen[kTiles];  // max cosine to the picks so far (-inf before the first)
-  uint32_t live = 0;
-  int nbad = 0;
-#pragma unroll
-  for (int j = 0; j < kTiles; ++j) {
-    const int c = cpos(j);
-    int32_t item = c < C ? cand_items[u * C + c] : -1;
-    if (item >= 0 && (int64_t)item >= n_items) {  // out of range: counted, never picked
-      nbad += h == 0 ? 1 : 0;
-      item = -1;
-    }
-    const bool ok = item >= 0;
-    live |= (ok ? 1u : 0u) << j;
-    const float sc = ok ? cand_scores[u * C + c] : 0.f;
-    if (h == 0) {
-      s_citem[c] = item;
-      s_cscore[cidx(j)] = sc;
-    }
-    pen[j] = -INFINITY;
-    const uint4* src = reinterpret_cast<const uint4*>(E + (int64_t)(ok ? item : 0) * D) + h;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) brow[j][s] = __builtin_bit_cast(bf16x8, src[2 * s]);
-  }
-  if (nbad && err) atomicAdd(err, nbad);
-#pragma unroll
-  for (int j = 0; j < kTiles; ++j) {
-    float nsq = 0.f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const uint4 v = __builtin_bit_cast(uint4, brow[j][s]);
-      const uint32_t pr[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bf16x2 a = __builtin_bit_cast(bf16x2, pr[e]);
-        nsq = __builtin_amdgcn_fdot2_f32_bf16(a, a, nsq, false);
-      }
-    }
-    nsq += __shfl_xor(nsq, 32);  // the two half-rows of the candidate
-    if (h == 0) s_cinv[cidx(j)] = 1.f / sqrtf(nsq);
-  }
-  __syncthreads();
-  MG_ADD(kMgLoad, t_kernel);
-
-  int t = 0;
-  // every batch picks at least once (its best probe beats BOUND by
-  // construction), so k_out batches always suffice; the cap only bounds the
-  // loop should that invariant ever break
-  for (int batch = 0; t < k_out && batch <= k_out; ++batch) {
-    // Lane coordinates re-derived from an opaque copy of the thread id every
-    // batch: otherwise hipcc hoists dozens of per-lane LDS offsets out of the
-    // loop, and with 192 VGPRs of rows + columns resident they spill (and the
-    // reloads land inside the MFMA chain).
-    uint32_t tl = threadIdx.x;
-    asm volatile("" : "+v"(tl));
-    const int lane = (int)(tl & 63u), h = lane >> 5, q = lane & 31;
-    auto cpos = [&](int j) { return kWaves * (32 * j + q) + w; };
-    auto cidx = [&](int j) { return w * 128 + 32 * j + q; };
-    MG_T0(t_sel);
-
-    // ---- probes: the kPerWave best live candidates of this wave + its bound.
-    // Lane (q, h) ranks tiles 2h and 2h+1 (the two half-waves hold the same
-    // candidates; this way each is counted once). Key = ord(value) << 32 |
-    // ~position: (value desc, position asc), exact.
-    uint64_t kk[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float sc = s_cscore[w * 128 + 32 * (2 * h + i) + q];
-      uint64_t key = 0ull;
-#pragma unroll
-      for (int j = 0; j < kTiles; ++j) {
-        if (j == 2 * h + i && ((live >> j) & 1u)) {
-          // the value every phase computes: lambda*s before the first pick,
-          // then fma(-mu, pen, lambda*s)
-          const float val = t == 0 ? lambda * sc : fmaf(-mu, pen[j], lambda * sc);
-          key = dr::make_key(val, (uint32_t)cpos(j));
-        }
-      }
-      kk[i] = key;
-      (void)sc;
-    }
-    int pc[kPerWave];  // positions of this wave's probes (uniform; -1 = none)
-    // per lane: probe slot + 1 of its candidate in tile j at bits 8j .. 8j+7
-    uint32_t myslot = 0u;
-#pragma unroll
-    for (int m = 0; m <= kPerWave; ++m) {
-      const uint64_t lb = dr::umax64(kk[0], kk[1]);  // this lane's best key
-      const uint32_t hi = (uint32_t)(lb >> 32);
-      const uint32_t mh = wmax_u32<64>(hi);  // best value (ord); 0 = no live key left
-      uint64_t best = 0ull;
-      if (mh != 0u) {
-        const uint64_t bal = __ballot(hi == mh);
-        if (__popcll(bal) == 1) best = dr::readlane_u64(lb, __builtin_ctzll(bal));
-        else best = wave_max_u64(hi == mh ? lb : 0ull);  // equal values: lowest position
-      }
-      if (m == kPerWave) {
-        if (lane == 0) s_wbound[w] = best;
-        break;
-      }
-      const int slot = w * kPerWave + m;
-      pc[m] = __builtin_amdgcn_readfirstlane(best != 0ull ? (int)dr::key_item(best) : -1);
-      if (best != 0ull) {
-        kk[0] = kk[0] == best ? 0ull : kk[0];
-        kk[1] = kk[1] == best ? 0ull : kk[1];
-        const int pj = (pc[m] >> 3) >> 5, pq = (pc[m] >> 3) & 31;
-        if (q == pq) myslot |= (uint32_t)(slot + 1) << (8 * pj);
-      }
-      if (lane == 0) s_pcand[slot] = pc[m];
-    }
-    MG_ADD(kMgSelect, t_sel);
-    MG_T0(t_stage);
-    // the owners of each probe (lanes of its tile column, both halves) stage
-    // its row and state
-#pragma unroll
-    for (int j = 0; j < kTiles; ++j) {
-      const int sl = (int)((myslot >> (8 * j)) & 255u) - 1;
-      if (sl >= 0) {
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-          s_prow[sl * CPR + ((2 * s + h) ^ (sl & SWM))] = __builtin_bit_cast(uint4, brow[j][s]);
-        if (h == 0) {
-          s_pitem[sl] = s_citem[cpos(j)];
-          s_pinv[sl] = s_cinv[cidx(j)];
-          s_pscore[sl] = s_cscore[cidx(j)];
-          s_ppen[sl] = pen[j];
-        }
-      }
-    }
-    MG_T0(t_sbar);
-    lds_barrier();
-    MG_ADD(kMgStageBar, t_sbar);
-    uint64_t bound = 0ull;
-#pragma unroll
-    for (int i = 0; i < kWaves; ++i) bound = dr::umax64(bound, s_wbound[i]);
-    MG_ADD(kMgStage, t_stage);
-    MG_T0(t_mma);
-
-    // ---- MFMA: dot(probe p, candidate) for the 32 probes x this wave's 128
-    // candidates, four independent accumulator chains; the columns stay here
-    // until the fold. Register r of tile j holds probe p(r) = 8*(r/4) + 4h + r%4.
-    f32x16 acc[kTiles];
-#pragma unroll
-    for (int j = 0; j < kTiles; ++j) acc[j] = f32x16{};
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const bf16x8 a = __builtin_bit_cast(bf16x8, s_prow[q * CPR + ((2 * s + h) ^ (q & SWM))]);
-#pragma unroll
-      for (int j = 0; j < kTiles; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, brow[j][s], acc[j], 0, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < kTiles; ++j) {
-      const float ci = s_cinv[cidx(j)];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 v = *reinterpret_cast<const float4*>(&s_pinv[8 * g + 4 * h]);
-        const float pv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[j][4 * g + e] = acc[j][4 * g + e] * ci * pv[e];
-      }
-    }
-    MG_T0(t_gt);
-    // the owners of probe b write row b of s_gt (their column of the batch)
-#pragma unroll
-    for (int j = 0; j < kTiles; ++j) {
-      const int sl = (int)((myslot >> (8 * j)) & 255u) - 1;
-      if (sl >= 0) {
-        float* row = &s_gt[sl * GTS + 4 * h];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) row[8 * (r >> 2) + (r & 3)] = acc[j][r];
-      }
-    }
-    MG_ADD(kMgGt, t_gt);
-    MG_ADD(kMgMma, t_mma);
-    MG_T0(t_sync1);
-    lds_barrier();
-    MG_ADD(kMgSync1, t_sync1);
-    MG_T0(t_rounds);
-
-    // ---- fast rounds over the probes: wave 0 alone (the other waves wait at
-    // the batch-end barrier). Lane a < 32 holds probe a. The argmax is a 32-bit
-    // max of ord(value) (fused DPP); an exact tie of values falls back to the
-    // lowest candidate position, so the pick is the (value desc, position asc) max.
-#if DR_MMR_ALLWAVES
-    // every wave runs the (identical) rounds: t and the picked mask stay in
-    // registers, so no post-round barrier or LDS broadcast is needed
-    uint32_t picked = 0;
-    {
-#else
-    if (w == 0) {
-#endif
-      const int pa = lane < kProbes ? s_pcand[lane] : -1;
-      const int pitem = lane < kProbes ? s_pitem[lane] : -1;
-      const float lsa = lambda * (lane < kProbes ? s_pscore[lane] : 0.f);
-      float pna = lane < kProbes ? s_ppen[lane] : 0.f;
-      const int gbase = (lane & 31) * GTS;
-      const uint32_t bhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bound >> 32));
-      const uint32_t blo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bound);
-      const bool first = t == 0;  // round 0 ranks without the max term: one pick, then a new batch
-      bool alive = pa >= 0;
-#if !DR_MMR_ALLWAVES
-      uint32_t picked = 0;
-#endif
-      while (t < k_out) {
-        const float val = first ? lsa : fmaf(-mu, pna, lsa);
-        const uint32_t ov = alive ? dr::f32_to_ord(val) : 0u;  // live ords are > 0
-        const uint32_t m = wmax_u32<32>(ov);
-        if (m == 0u) {  // no live probe
-          if ((bhi | blo) != 0u) break;
-          if (w == 0 && lane == 0) s_out[t] = -1;  // no live candidate left
-          ++t;
-          continue;
-        }
-        uint64_t bal = __ballot(ov == m);
-        if (__popcll(bal) > 1) {  // equal values: lowest candidate position wins
-          const uint32_t mp = wave_min_u32_32(ov == m ? (uint32_t)pa : 0xffffffffu);
-          bal = __ballot(ov == m && (uint32_t)pa == mp);
-        }
-        const int pk = __builtin_ctzll(bal);
-        const uint32_t npos = ~(uint32_t)__builtin_amdgcn_readlane(pa, pk);
-        if (m < bhi || (m == bhi && npos <= blo)) break;  // a non-probe may be better
-        const float g = s_gt[gbase + pk];  // issued ahead of the bookkeeping
-        if (w == 0 && lane == pk) s_out[t] = pitem;
-        picked |= 1u << pk;
-        alive = alive && lane != pk;
-        ++t;
-        if (first) break;
-        pna = fmaxf(pna, g);
-      }
-#if !DR_MMR_ALLWAVES
-      if (lane == 0) {
-        s_round[0] = t;
-        s_round[1] = (int)picked;
-      }
-#endif
-    }
-    MG_ADD(kMgRounds, t_rounds);
-    MG_T0(t_sync2);
-#if DR_MMR_ALLWAVES
-    t = __builtin_amdgcn_readfirstlane(t);
-    picked = (uint32_t)__builtin_amdgcn_readfirstlane((int)picked);
-#else
-    lds_barrier();
-    t = s_round[0];
-    const uint32_t picked = (uint32_t)s_round[1];
-#endif
-    MG_ADD(kMgSync2, t_sync2);
-    MG_T0(t_fold);
-
-    // ---- batch end: fold the picked columns into every candidate's max term,
-    // straight from the accumulators (lane half h holds probes 8i + 4h + e)
-    const uint32_t pm = picked >> (4 * h);
-#pragma unroll
-    for (int j = 0; j < kTiles; ++j) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if ((pm >> (8 * (r >> 2) + (r & 3))) & 1u) mx = fmaxf(mx, acc[j][r]);
-      pen[j] = fmaxf(pen[j], half_swap_max(mx));
-    }
-    // picked probes of this wave leave the live set
-#pragma unroll
-    for (int j = 0; j < kTiles; ++j) {
-      const int sl = (int)((myslot >> (8 * j)) & 255u) - 1;
-      if (sl >= 0 && ((picked >> sl) & 1u)) live &= ~(1u << j);
-    }
-    lds_barrier();  // s_prow / s_gt / s_wbound / s_pcand are rewritten by the next batch
-    MG_ADD(kMgFold, t_fold);
-#ifdef DR_MMR_DIAG
-    dg[kMgBatches] += 1;
-#endif
-  }
-  __syncthreads();
-  for (int i = tid; i < k_out; i += kThreads) out_items[u * k_out + i] = s_out[i];
-#ifdef DR_MMR_DIAG
-  MG_ADD(kMgTotal, t_kernel);
-  if (lane == 0)
-    for (int i = 0; i < kMgSlots; ++i) atomicAdd(&g_mmr_diag[w][i], (unsigned long long)dg[i]);
-#endif
-}
-#endif  // DR_MMR_LEGACY
 
 // ---------------------------------------------------------------------------
 // Round-3 layout: MFMA work proportional to the PICKS, not to the probes.
@@ -510,7 +126,7 @@ typedef float f32x32 __attribute__((ext_vector_type(32)));
 template <int D>
 __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
     const int32_t* __restrict__ cand_items, const float* __restrict__ cand_scores, int C,
-    const __bf16* __restrict__ E, int64_t n_items, int k_out, float lambda,
+    const __bf16* __restrict__ E, int64_t n_items, int64_t n_users, int k_out, float lambda,
     int32_t* __restrict__ out_items, int32_t* __restrict__ err) {
   constexpr int KS = D / 16;  // MFMA k-steps per row
   constexpr int CPR = D / 8;  // 16-B chunks per row
@@ -529,20 +145,85 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
   __shared__ uint64_t s_wbound[kWaves];
   __shared__ int s_state[5];  // rounds done, picks this batch, picked mask lo / hi, forced pick
   __shared__ int s_out[kMaxC];
+  // Prefetch of the workgroup's next user (persistent grid), by LDS-DMA while
+  // this user runs: its ids and scores, and the rows of candidate tile 0 of
+  // every wave (256 rows; chunk c of row r at r*CPR + (c ^ (r & SWM)))
+  __shared__ int s_nitem[kMaxC];
+  __shared__ float s_nscore[kMaxC];
+  __shared__ uint4 s_pf[kWaves * 32 * CPR];
   auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  auto lds_addr = [](const void* p) {
+    return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+  };
 
-  const int64_t u = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, q = lane & 31;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const float mu = 1.f - lambda;
-  auto cpos = [&](int j) { return kWaves * (32 * j + q) + w; };
-  auto cidx = [&](int j) { return w * 128 + 32 * j + q; };
 #ifdef DR_MMR_DIAG
   uint64_t dg[kMgSlots] = {};
-#endif
   MG_T0(t_kernel);
+#endif
 
-  // ---- candidate rows -> B fragments (as in the round-2 kernel)
+  // Persistent grid: workgroup b runs users b, b + G, ...; user b + G's ids,
+  // scores and tile-0 rows arrive by LDS-DMA while user b runs.
+  const int64_t G = gridDim.x;
+  for (int64_t u = blockIdx.x; u < n_users; u += G) {
+  // lane coordinates from an opaque copy of the thread id at every user:
+  // otherwise hipcc hoists per-lane addresses out of the user loop and spills
+  uint32_t tl0 = threadIdx.x;
+  asm volatile("" : "+v"(tl0));
+  const int tid = (int)tl0, lane = tid & 63, h = lane >> 5, q = lane & 31;
+  auto cpos = [&](int j) { return kWaves * (32 * j + q) + w; };
+  auto cidx = [&](int j) { return w * 128 + 32 * j + q; };
+  // ids and scores of user un: 2 x 16 LDS-DMA blocks of 64 words, 2 + 2 per
+  // wave (entries past C repeat entry C - 1: never read)
+  auto issue_ids = [&](int64_t un) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int e = (2 * w + b) * 64 + lane;
+      const int64_t src = un * C + (e < C ? e : C - 1);
+      const uint32_t m0i = lds_addr(s_nitem) + (uint32_t)(2 * w + b) * 256u;
+      const uint32_t m0s = lds_addr(s_nscore) + (uint32_t)(2 * w + b) * 256u;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
+                   : : "v"(cand_items + src), "s"(m0i) : "memory", "m0");
+      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
+                   : : "v"(cand_scores + src), "s"(m0s) : "memory", "m0");
+#pragma clang diagnostic pop
+    }
+  };
+  // tile-0 rows of the next user (its ids in s_nitem): 256 * CPR 16-B chunks,
+  // 64 per DMA instruction; an empty or out-of-range id loads row 0 (never used)
+  auto issue_rows = [&]() {
+    constexpr int PER = 32 * CPR / 64;  // instructions per wave
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int blk = w * PER + k;
+      const int i = blk * 64 + lane;
+      const int r = i / CPR, c = (i % CPR) ^ (r & SWM);
+      const int32_t it = s_nitem[kWaves * (r & 31) + (r >> 5)];
+      const int64_t row = (it >= 0 && (int64_t)it < n_items) ? it : 0;
+      const __bf16* src = E + row * D + c * 8;
+      const uint32_t m0 = lds_addr(s_pf) + (uint32_t)blk * 1024u;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                   : : "v"(src), "s"(m0) : "memory", "m0");
+#pragma clang diagnostic pop
+    }
+  };
+  auto wait_dma = [] { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+
+  const bool pre = u != (int64_t)blockIdx.x;  // ids, scores and tile-0 rows prefetched
+  if (pre) {
+    wait_dma();
+    __syncthreads();
+  }
+#ifdef DR_MMR_DIAG
+  MG_T0(t_user);
+#endif
+
+  // ---- candidate rows -> B fragments (tile 0 from the prefetch, if any)
   bf16x8 brow[kTiles][KS];
   float pen[kTiles];
   uint32_t live = 0;
@@ -550,22 +231,29 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
 #pragma unroll
   for (int j = 0; j < kTiles; ++j) {
     const int c = cpos(j);
-    int32_t item = c < C ? cand_items[u * C + c] : -1;
+    int32_t item = c < C ? (pre ? s_nitem[c] : cand_items[u * C + c]) : -1;
     if (item >= 0 && (int64_t)item >= n_items) {
       nbad += h == 0 ? 1 : 0;
       item = -1;
     }
     const bool ok = item >= 0;
     live |= (ok ? 1u : 0u) << j;
-    const float sc = ok ? cand_scores[u * C + c] : 0.f;
+    const float sc = ok ? (pre ? s_nscore[c] : cand_scores[u * C + c]) : 0.f;
     if (h == 0) {
       s_citem[c] = item;
       s_cscore[cidx(j)] = sc;
     }
     pen[j] = -INFINITY;
-    const uint4* src = reinterpret_cast<const uint4*>(E + (int64_t)(ok ? item : 0) * D) + h;
+    if (j == 0 && pre) {
+      const int r = w * 32 + q;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) brow[j][s] = __builtin_bit_cast(bf16x8, src[2 * s]);
+      for (int s = 0; s < KS; ++s)
+        brow[0][s] = __builtin_bit_cast(bf16x8, s_pf[r * CPR + ((2 * s + h) ^ (r & SWM))]);
+    } else {
+      const uint4* src = reinterpret_cast<const uint4*>(E + (int64_t)(ok ? item : 0) * D) + h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) brow[j][s] = __builtin_bit_cast(bf16x8, src[2 * s]);
+    }
   }
   if (nbad && err) atomicAdd(err, nbad);
 #pragma unroll
@@ -585,7 +273,9 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
     if (h == 0) s_cinv[cidx(j)] = 1.f / sqrtf(nsq);
   }
   __syncthreads();
-  MG_ADD(kMgLoad, t_kernel);
+  MG_ADD(kMgLoad, t_user);
+  const bool more = u + G < n_users;
+  if (more) issue_ids(u + G);  // s_nitem / s_nscore are free from here
 
   // Fold the np picks of s_plist (their rows staged in s_prow, 1/|e| in
   // s_lpinv) into every candidate's max term: rows of A = the picks in pick
@@ -606,19 +296,29 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
         for (int j = 0; j < kTiles; ++j)
           acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, brow[j][s], acc[j], 0, 0, 0);
       }
-      float pv[16];
+      // 1/|pick| per register pair; NaN for rows past the picks, whose
+      // products (NaN) the max ignores: no per-score select
+      f32x2 pv2[8];
 #pragma unroll
       for (int gg = 0; gg < 4; ++gg) {
         const float4 v = *reinterpret_cast<const float4*>(&s_lpinv[i0 + 8 * gg + 4 * h]);
-        pv[4 * gg + 0] = v.x; pv[4 * gg + 1] = v.y; pv[4 * gg + 2] = v.z; pv[4 * gg + 3] = v.w;
+        const int r0 = 8 * gg + 4 * h;
+        const float nan = __builtin_nanf("");
+        pv2[2 * gg] = f32x2{r0 < nrow ? v.x : nan, r0 + 1 < nrow ? v.y : nan};
+        pv2[2 * gg + 1] = f32x2{r0 + 2 < nrow ? v.z : nan, r0 + 3 < nrow ? v.w : nan};
       }
+      // cos = (acc * 1/|c|) * 1/|p|, the Gram's operand order, two scores per
+      // v_pk_mul_f32
 #pragma unroll
       for (int j = 0; j < kTiles; ++j) {
         const float ci = s_cinv[cidx(j)];
+        const f32x2 c2 = {ci, ci};
         float mx = -INFINITY;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (8 * (r >> 2) + 4 * h + (r & 3) < nrow) mx = fmaxf(mx, acc[j][r] * ci * pv[r]);
+        for (int r = 0; r < 16; r += 2) {
+          const f32x2 cs = (f32x2{acc[j][r], acc[j][r + 1]} * c2) * pv2[r / 2];
+          mx = fmaxf(mx, fmaxf(cs.x, cs.y));
+        }
         pen[j] = fmaxf(pen[j], half_swap_max(mx));
       }
     }
@@ -667,8 +367,13 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
     }
     lds_barrier();  // s_wbound / s_prow are rewritten by the first batch
   }
+  if (more) {  // the next user's ids are in (every wave's DMA + a barrier): its tile-0 rows
+    wait_dma();
+    __syncthreads();
+    issue_rows();
+  }
   for (int batch = 0; t < k_out && batch <= k_out; ++batch) {
-    uint32_t tl = threadIdx.x;  // opaque lane coordinates (see mmr_batch_kernel)
+    uint32_t tl = threadIdx.x;  // opaque lane coordinates: else hipcc hoists per-lane LDS offsets and spills them
     asm volatile("" : "+v"(tl));
     const int lane = (int)(tl & 63u), h = lane >> 5, q = lane & 31;
     auto cpos = [&](int j) { return kWaves * (32 * j + q) + w; };
@@ -732,7 +437,16 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
       }
     }
     myslot |= (uint32_t)__shfl_xor((int)myslot, 32);  // the other half-wave holds the same rows
-    if (lane < kPPW && lane >= nprobe) s_pcand[w * kPPW + lane] = -1;
+    if (lane < kPPW && lane >= nprobe) {
+      // an empty slot: zero row and 1/|e| = 0, so its Gram entries are 0
+      // (finite) and the rounds' max terms stay finite without a select
+      const int sl = w * kPPW + lane;
+      s_pcand[sl] = -1;
+      s_pinv[sl] = 0.f;
+      s_ppen[sl] = 0.f;
+#pragma unroll
+      for (int c = 0; c < CPR; ++c) s_prow[sl * CPR + c] = uint4{0u, 0u, 0u, 0u};
+    }
     uint64_t wb = 0ull;  // the wave's bound: value p9 at its lowest position among the rest
     if (p9 != 0u) {
       uint32_t mp = 0xffffffffu;
@@ -805,7 +519,11 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
     // on one, sits in the chain.
     if (w == 0) {
       const int pa = s_pcand[lane];
-      const float lsa = lambda * s_pscore[lane];
+      // +0: lambda * s is never -0, so no value below is -0 either (an fma
+      // with a nonzero or +0 addend), and the key order needs no -0 fix-up
+      // in the chain. An empty or picked slot has lsa = -inf: its value is
+      // -inf, key kDead, below every live value.
+      float lsa = pa >= 0 ? lambda * s_pscore[lane] + 0.0f : -INFINITY;
       float pna = s_ppen[lane];
       f32x32 g0, g1;  // this probe's Gram row, indexed by the (uniform) pick slot
       {
@@ -817,43 +535,119 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
           g1[4 * i + 0] = b.x; g1[4 * i + 1] = b.y; g1[4 * i + 2] = b.z; g1[4 * i + 3] = b.w;
         }
       }
-      // values in the key order's high word: ord(v) (0 = not live)
-      auto ordv = [](float v) {
-        const uint32_t u = __float_as_uint(v + 0.0f);  // -0 -> +0
-        return u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
-      };
+      // values in the key order's high word
+      auto ordv = [](float v) { return __float_as_uint(v) ^ ((uint32_t)((int32_t)__float_as_uint(v) >> 31) | 0x80000000u); };
+      constexpr uint32_t kDead = 0x007fffffu;  // ordv(-inf)
       const uint32_t bhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bound >> 32));
       const uint32_t blo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bound);
+      // a real bound's value is finite (bhi > kDead); bhi = 0: no candidate
+      // outside the probes. A round stops at m <= bcut, except a tie with a
+      // real bound that the probe wins by a lower position.
+      const uint32_t bcut = bhi > kDead ? bhi : kDead;
       // t >= 1 here whenever a live candidate exists (the first pick is made
       // before the batches: values only fall from then on, which the bound
       // needs), so every live max term is finite
-      bool alive = pa >= 0;
-      uint32_t cur = alive ? ordv(fmaf(-mu, pna, lsa)) : 0u;
+      uint32_t cur = ordv(fmaf(-mu, pna, lsa));
       int rec_slot = -1;  // lane i: probe slot of pick i of this batch
       const int t0 = t, nr = k_out - t;
       int np = 0;
       uint64_t picked = 0;
       uint32_t m = 0u;
+      // The chain of a round: wave max (fused DPP) -> ballot -> pick -> Gram
+      // entry (SGPR-indexed register read) -> max term -> key. The stop tests
+      // and the tie resolution sit off the common path (one scalar compare).
+      const float nmu = -mu, ninf = -INFINITY;
       for (;;) {
-        m = wmax_u32<64>(cur);
-        if (m == 0u) break;  // no live probe: a non-probe is next, or nothing is left
-        uint64_t bal = __ballot(cur == m);
-        if (bal & (bal - 1)) {  // equal values: lowest candidate position wins
+        // Common rounds in one asm loop: no tie, no stop test passed, list
+        // not full. status 1: the list is full; 2: the slow path below
+        // (m <= bcut, or equal values) with m and bal = ballot(cur == m).
+        // The Gram row sits in v[2:65] (g0, g1), read by an SGPR-indexed
+        // v_mov (s_set_gpr_idx_on). Wait states as hipcc schedules these
+        // pairs: 2 between a DPP source write and the DPP, and between a
+        // VALU mask write and its v_cndmask.
+        uint64_t bal, sel_, vm_, sh_;
+        int status, sc_, spk_, spi_;
+        float vt_, vga_, vgb_, vpk_;
+        asm volatile(
+            "L_rt_%=:\n\t"
+            "s_nop 1\n\t"
+            "v_max_u32_dpp %[t], %[cur], %[cur] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "s_nop 1\n\t"
+            "v_max_u32_dpp %[t], %[t], %[t] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "s_nop 1\n\t"
+            "v_max_u32_dpp %[t], %[t], %[t] row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "s_nop 1\n\t"
+            "v_max_u32_dpp %[t], %[t], %[t] row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "s_nop 1\n\t"
+            "v_max_u32_dpp %[t], %[t], %[t] row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+            "s_nop 1\n\t"
+            "v_max_u32_dpp %[t], %[t], %[t] row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+            "s_nop 1\n\t"
+            "v_readlane_b32 %[m], %[t], 63\n\t"
+            "s_cmp_le_u32 %[m], %[bcut]\n\t"
+            "s_nop 0\n\t"
+            "v_cmp_eq_u32_e64 %[bal], %[m], %[cur]\n\t"
+            "s_cbranch_scc1 L_rs_%=\n\t"
+            "s_bcnt1_i32_b64 %[c], %[bal]\n\t"
+            "s_cmp_gt_u32 %[c], 1\n\t"
+            "s_cbranch_scc1 L_rs_%=\n\t"
+            "s_ff1_i32_b64 %[pk], %[bal]\n\t"
+            "s_and_b32 %[pi], %[pk], 31\n\t"
+            "s_cmp_lt_u32 %[pk], 32\n\t"
+            "s_cselect_b64 %[sel], -1, 0\n\t"
+            "s_set_gpr_idx_on %[pi], gpr_idx(SRC0)\n\t"
+            "v_mov_b32 %[ga], v2\n\t"
+            "v_mov_b32 %[gb], v34\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "v_cmp_ne_u32_e64 %[vm], %[pk], %[lane]\n\t"
+            "v_mov_b32 %[pkv], %[pk]\n\t"
+            "v_cndmask_b32_e64 %[ga], %[gb], %[ga], %[sel]\n\t"
+            "v_max_f32 %[pna], %[ga], %[pna]\n\t"
+            "v_cndmask_b32_e64 %[lsa], %[ninf], %[lsa], %[vm]\n\t"
+            "v_fma_f32 %[t], %[nmu], %[pna], %[lsa]\n\t"
+            "v_cmp_eq_u32_e64 %[vm], %[np], %[lane]\n\t"
+            "v_ashrrev_i32 %[ga], 31, %[t]\n\t"
+            "v_bitop3_b32 %[cur], %[ga], %[t], %[c80] bitop3:0x36\n\t"
+            "s_lshl_b64 %[sh], 1, %[pk]\n\t"
+            "s_or_b64 %[pkd], %[pkd], %[sh]\n\t"
+            "v_cndmask_b32_e64 %[rec], %[rec], %[pkv], %[vm]\n\t"
+            "s_add_u32 %[np], %[np], 1\n\t"
+            "s_cmp_lt_u32 %[np], %[nr]\n\t"
+            "s_cbranch_scc1 L_rt_%=\n\t"
+            "s_mov_b32 %[st], 1\n\t"
+            "s_branch L_re_%=\n"
+            "L_rs_%=:\n\t"
+            "s_mov_b32 %[st], 2\n"
+            "L_re_%=:"
+            : [cur] "+v"(cur), [pna] "+v"(pna), [lsa] "+v"(lsa), [rec] "+v"(rec_slot),
+              [np] "+s"(np), [pkd] "+s"(picked), [st] "=s"(status), [m] "=s"(m), [bal] "=s"(bal),
+              [t] "=&v"(vt_), [ga] "=&v"(vga_), [gb] "=&v"(vgb_), [pkv] "=&v"(vpk_), [c] "=&s"(sc_),
+              [pk] "=&s"(spk_), [pi] "=&s"(spi_), [sel] "=&s"(sel_), [vm] "=&s"(vm_), [sh] "=&s"(sh_)
+            : [g0] "{v[2:33]}"(g0), [g1] "{v[34:65]}"(g1), [bcut] "s"(bcut), [nr] "s"(nr),
+              [lane] "v"(lane), [nmu] "v"(nmu), [ninf] "v"(ninf), [c80] "s"(0x80000000u)
+            : "scc");
+        if (status == 1) break;  // the list is full
+        // slow path (rare): a stop test, or equal values at the top
+        if (m <= bcut) {
+          if (m != bhi) break;  // below a real bound, or no live probe (m = kDead)
+          const uint32_t mp = wave_min_u32_64(cur == m ? (uint32_t)pa : 0xffffffffu);
+          if (mp >= ~blo) break;  // the bound's candidate has the lower position
+          bal = __ballot(cur == m && (uint32_t)pa == mp);
+        } else {  // equal values: lowest candidate position wins
           const uint32_t mp = wave_min_u32_64(cur == m ? (uint32_t)pa : 0xffffffffu);
           bal = __ballot(cur == m && (uint32_t)pa == mp);
         }
         const int pk = __builtin_amdgcn_readfirstlane(__builtin_ctzll(bal));
-        const uint32_t npos = ~(uint32_t)__builtin_amdgcn_readlane(pa, pk);
-        // stop when a non-probe may be better, or the list is full
-        if (m < bhi || (m == bhi && npos <= blo) || np == nr) break;
         const float ga = g0[pk & 31], gb = g1[pk & 31];
         const float g = pk < 32 ? ga : gb;
+        lsa = lane == pk ? -INFINITY : lsa;
         rec_slot = lane == np ? pk : rec_slot;
         picked |= 1ull << pk;
-        ++np;
-        alive = alive && lane != pk;
-        pna = g > pna ? g : pna;  // a select: fmaxf would canonicalize both inputs first
-        cur = alive ? ordv(fmaf(-mu, pna, lsa)) : 0u;
+        float nx;  // max(pna, g): one v_max_f32 (no canonicalizing copies; no NaN here)
+        asm("v_max_f32 %0, %1, %2" : "=v"(nx) : "v"(g), "v"(pna));
+        pna = nx;
+        cur = ordv(fmaf(-mu, pna, lsa));
+        if (++np == nr) break;  // the list is full
       }
       t += np;
       if (lane < np) {
@@ -861,7 +655,7 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
         s_plist[lane] = rec_slot;
         s_lpinv[lane] = s_pinv[rec_slot];
       }
-      if (m == 0u && (bhi | blo) == 0u) {  // no live candidate left: the rest are -1
+      if (m == kDead && bhi == 0u) {  // no live candidate left: the rest are -1
         for (int i = t + lane; i < k_out; i += 64) s_out[i] = -1;
         t = k_out;
       }
@@ -929,6 +723,7 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
   }
   __syncthreads();
   for (int i = tid; i < k_out; i += kThreads) out_items[u * k_out + i] = s_out[i];
+  }  // users
 #ifdef DR_MMR_DIAG
   MG_ADD(kMgTotal, t_kernel);
   if (lane == 0)
@@ -962,15 +757,21 @@ extern "C" int dr_mmr_rerank(const int32_t* cand_items, const float* cand_scores
   if (n_users == 0) return DR_OK;
   DR_CHECK_ARG(cand_items && cand_scores && item_table && out_items, "null pointer");
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)n_users);
-#if DR_MMR_LEGACY
-#define DR_MMR_KERNEL mmr_batch_kernel
-#else
-#define DR_MMR_KERNEL mmr_pick_kernel
-#endif
+  // persistent grid: one workgroup per CU (a user's rows take half the
+  // register file), each looping over users and prefetching the next one
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      cus = n;
+    else
+      cus = 256;
+  }
+  const dim3 grid((unsigned)(n_users < cus ? n_users : cus));
 #define DR_MMR(DD)                                                                            \
-  hipLaunchKernelGGL(DR_MMR_KERNEL<DD>, grid, dim3(kThreads), 0, s, cand_items, cand_scores,    \
-                     C, (const __bf16*)item_table, n_items, k_out, lambda, out_items, err)
+  hipLaunchKernelGGL(mmr_pick_kernel<DD>, grid, dim3(kThreads), 0, s, cand_items, cand_scores,  \
+                     C, (const __bf16*)item_table, n_items, n_users, k_out, lambda, out_items, err)
   switch (d) {
     case 64: DR_MMR(64); break;
     case 128: DR_MMR(128); break;
