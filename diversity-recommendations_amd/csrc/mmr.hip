@@ -120,6 +120,7 @@ __device__ __forceinline__ uint32_t wmax_u32(uint32_t v) {
 // probe are bit-identical to what the fold leaves in its max term: the picks
 // are exactly the eager greedy's on these fp32 cosines, as before.
 constexpr int kPP = 64;               // probes per batch
+
 constexpr int kPPW = kPP / kWaves;    // per wave
 typedef float f32x32 __attribute__((ext_vector_type(32)));
 
@@ -408,12 +409,39 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
       r_sc[i] = sc;
       r_pen[i] = pn;
     }
-    uint32_t p9 = 0u;  // largest p with at least kPPW + 1 values >= p (0: fewer live)
-    for (int bit = 31; bit >= 0; --bit) {
-      const uint32_t c = p9 | (1u << bit);
-      const int n = __popcll(__ballot(v2[0] >= c)) + __popcll(__ballot(v2[1] >= c));
-      p9 = n >= kPPW + 1 ? c : p9;
+    // Probe threshold pthr: the wave's probes are its live values > pthr (at
+    // most kPPW of them), pthr the (kPPW + 1)-th largest value, found by a
+    // radix select bit by bit, both ballots of a step into their own SGPR
+    // pairs (hipcc serialises them through VCC). The selection is SALU-bound
+    // (the eight waves share the CU's scalar unit); skipping the live values'
+    // common prefix and stopping 8 bits short measured slower (64.3 -> 65.7 ms).
+    static_assert(kPPW + 1 == 9, "the asm below counts against 8");
+    auto radix_step = [&](uint32_t p, uint32_t bit) {
+      uint64_t ba_, bb_;
+      uint32_t c_, na_, nb_;
+      asm volatile(
+          "s_or_b32 %[c], %[p], %[bit]\n\t"
+          "v_cmp_le_u32_e64 %[ba], %[c], %[v0]\n\t"
+          "v_cmp_le_u32_e64 %[bb], %[c], %[v1]\n\t"
+          "s_bcnt1_i32_b64 %[na], %[ba]\n\t"
+          "s_bcnt1_i32_b64 %[nb], %[bb]\n\t"
+          "s_add_u32 %[na], %[na], %[nb]\n\t"
+          "s_cmp_gt_u32 %[na], 8\n\t"
+          "s_cselect_b32 %[p], %[c], %[p]"
+          : [p] "+s"(p), [ba] "=&s"(ba_), [bb] "=&s"(bb_), [c] "=&s"(c_), [na] "=&s"(na_),
+            [nb] "=&s"(nb_)
+          : [bit] "s"(bit), [v0] "v"(v2[0]), [v1] "v"(v2[1])
+          : "scc");
+      return p;
+    };
+    uint32_t pthr;
+    {
+      uint32_t p = 0u;  // the largest p with at least kPPW + 1 values >= p (0: fewer live)
+#pragma unroll
+      for (int bit = 31; bit >= 0; --bit) p = radix_step(p, 1u << bit);
+      pthr = p;
     }
+    const uint32_t p9 = pthr;
     const uint64_t b0 = __ballot(v2[0] > p9), b1 = __ballot(v2[1] > p9);
     const int n0 = __popcll(b0), nprobe = n0 + __popcll(b1);
     uint32_t myslot = 0u;  // per tile j: probe slot + 1 of this lane's candidate (bits 8j..)
@@ -447,17 +475,19 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
 #pragma unroll
       for (int c = 0; c < CPR; ++c) s_prow[sl * CPR + c] = uint4{0u, 0u, 0u, 0u};
     }
-    uint64_t wb = 0ull;  // the wave's bound: value p9 at its lowest position among the rest
-    if (p9 != 0u) {
+    // the wave's bound: the best value <= pthr, at its lowest position
+    uint64_t wb = 0ull;
+    const uint32_t bval = p9;  // p9 itself is a value (0: fewer than kPPW + 1 live)
+    if (bval != 0u) {
       uint32_t mp = 0xffffffffu;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        if (v2[i] == p9) {
+        if (v2[i] == bval) {
           const uint32_t pos = (uint32_t)(kWaves * (32 * (2 * h + i) + q) + w);
           mp = pos < mp ? pos : mp;
         }
       mp = wave_min_u32_64(mp);
-      wb = ((uint64_t)p9 << 32) | (uint32_t)~mp;
+      wb = ((uint64_t)bval << 32) | (uint32_t)~mp;
     }
     if (lane == 0) s_wbound[w] = wb;
     MG_ADD(kMgSelect, t_sel);
@@ -561,13 +591,14 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
         // Common rounds in one asm loop: no tie, no stop test passed, list
         // not full. status 1: the list is full; 2: the slow path below
         // (m <= bcut, or equal values) with m and bal = ballot(cur == m).
-        // The Gram row sits in v[2:65] (g0, g1), read by an SGPR-indexed
-        // v_mov (s_set_gpr_idx_on). Wait states as hipcc schedules these
-        // pairs: 2 between a DPP source write and the DPP, and between a
-        // VALU mask write and its v_cndmask.
-        uint64_t bal, sel_, vm_, sh_;
-        int status, sc_, spk_, spi_;
-        float vt_, vga_, vgb_, vpk_;
+        // The Gram row sits in v[2:65] (g0 then g1, contiguous by the operand
+        // constraints), read by one SGPR-indexed v_mov (s_set_gpr_idx_on);
+        // the pick's and the record's lane masks come from SALU shifts. Wait
+        // states as hipcc schedules these pairs: 2 between a DPP source write
+        // and the DPP.
+        uint64_t bal, vm_, sh_;
+        int status, sc_, spk_;
+        float vt_, vga_, vpk_;
         asm volatile(
             "L_rt_%=:\n\t"
             "s_nop 1\n\t"
@@ -592,23 +623,17 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
             "s_cmp_gt_u32 %[c], 1\n\t"
             "s_cbranch_scc1 L_rs_%=\n\t"
             "s_ff1_i32_b64 %[pk], %[bal]\n\t"
-            "s_and_b32 %[pi], %[pk], 31\n\t"
-            "s_cmp_lt_u32 %[pk], 32\n\t"
-            "s_cselect_b64 %[sel], -1, 0\n\t"
-            "s_set_gpr_idx_on %[pi], gpr_idx(SRC0)\n\t"
+            "s_set_gpr_idx_on %[pk], gpr_idx(SRC0)\n\t"
             "v_mov_b32 %[ga], v2\n\t"
-            "v_mov_b32 %[gb], v34\n\t"
             "s_set_gpr_idx_off\n\t"
-            "v_cmp_ne_u32_e64 %[vm], %[pk], %[lane]\n\t"
+            "s_lshl_b64 %[sh], 1, %[pk]\n\t"
+            "s_lshl_b64 %[vm], 1, %[np]\n\t"
             "v_mov_b32 %[pkv], %[pk]\n\t"
-            "v_cndmask_b32_e64 %[ga], %[gb], %[ga], %[sel]\n\t"
             "v_max_f32 %[pna], %[ga], %[pna]\n\t"
-            "v_cndmask_b32_e64 %[lsa], %[ninf], %[lsa], %[vm]\n\t"
+            "v_cndmask_b32_e64 %[lsa], %[lsa], %[ninf], %[sh]\n\t"
             "v_fma_f32 %[t], %[nmu], %[pna], %[lsa]\n\t"
-            "v_cmp_eq_u32_e64 %[vm], %[np], %[lane]\n\t"
             "v_ashrrev_i32 %[ga], 31, %[t]\n\t"
             "v_bitop3_b32 %[cur], %[ga], %[t], %[c80] bitop3:0x36\n\t"
-            "s_lshl_b64 %[sh], 1, %[pk]\n\t"
             "s_or_b64 %[pkd], %[pkd], %[sh]\n\t"
             "v_cndmask_b32_e64 %[rec], %[rec], %[pkv], %[vm]\n\t"
             "s_add_u32 %[np], %[np], 1\n\t"
@@ -621,10 +646,10 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
             "L_re_%=:"
             : [cur] "+v"(cur), [pna] "+v"(pna), [lsa] "+v"(lsa), [rec] "+v"(rec_slot),
               [np] "+s"(np), [pkd] "+s"(picked), [st] "=s"(status), [m] "=s"(m), [bal] "=s"(bal),
-              [t] "=&v"(vt_), [ga] "=&v"(vga_), [gb] "=&v"(vgb_), [pkv] "=&v"(vpk_), [c] "=&s"(sc_),
-              [pk] "=&s"(spk_), [pi] "=&s"(spi_), [sel] "=&s"(sel_), [vm] "=&s"(vm_), [sh] "=&s"(sh_)
+              [t] "=&v"(vt_), [ga] "=&v"(vga_), [pkv] "=&v"(vpk_), [c] "=&s"(sc_),
+              [pk] "=&s"(spk_), [vm] "=&s"(vm_), [sh] "=&s"(sh_)
             : [g0] "{v[2:33]}"(g0), [g1] "{v[34:65]}"(g1), [bcut] "s"(bcut), [nr] "s"(nr),
-              [lane] "v"(lane), [nmu] "v"(nmu), [ninf] "v"(ninf), [c80] "s"(0x80000000u)
+              [nmu] "v"(nmu), [ninf] "v"(ninf), [c80] "s"(0x80000000u)
             : "scc");
         if (status == 1) break;  // the list is full
         // slow path (rare): a stop test, or equal values at the top
@@ -726,7 +751,7 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
   }  // users
 #ifdef DR_MMR_DIAG
   MG_ADD(kMgTotal, t_kernel);
-  if (lane == 0)
+  if ((threadIdx.x & 63) == 0)
     for (int i = 0; i < kMgSlots; ++i) atomicAdd(&g_mmr_diag[w][i], (unsigned long long)dg[i]);
 #endif
 }
