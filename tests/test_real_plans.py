@@ -286,3 +286,55 @@ def test_config2_plan_1m_x_1m_d64_exact():
                                      256 * 2048 + rng.choice(U_n - 256 * 2048, 400, replace=False)]))
     _check(users, items, it, s, rows, k)
     _check(users, items, it, s, rng.choice(hot, 200, replace=False), k)
+
+
+def test_configs3_eight_way_item_shards_full_size():
+    """BASELINE configs[3] as bench.py --gpus 8 lays it out: the 10M-item
+    catalog row-sharded 8 ways (1.25M rows per rank), every rank scoring all
+    1M users against its shard from the global sample thresholds
+    (divrec.distributed.global_thresholds' rule: the whole catalog's rows at
+    the single-device stride, rank ks = guess_rank, threshold_below), then the
+    merge of the 8 thresholded partial lists and the exact fallback for users
+    the guess failed — thresholded_exchange's steps on one GPU, all eight
+    ranks' kernel calls in sequence (RCCL transport aside). Integer tables,
+    hot rows at sample positions for a user group (their guess fails and they
+    go through the fallback). Checked: the merged lists of ~1000 users, hot
+    ones included, against the exact top-k of the whole catalog."""
+    from divrec import distributed as D
+
+    U_n, I_n, d, k, S = 1_000_000, 10_000_000, 128, 100, 8
+    rng = np.random.default_rng(8)
+    users = _int_table_dev(U_n, d, 31)
+    items = _int_table_dev(I_n, d, 32)
+    st = D.sample_stride(I_n, k)
+    assert st == ops.score_topk_plan(U_n, I_n, torch.bfloat16, d, k)["sample_stride"] == 128
+    items[torch.arange(12, device=DEV) * st] = 3.0  # hot rows inside the sample, on shard 0
+    hot = np.unique(rng.choice(U_n, 2000, replace=False))
+    hot_t = torch.as_tensor(hot, device=DEV)
+    users[hot_t] = users[hot_t].abs()
+    # global thresholds from the whole catalog's sample (every rank's rows at j * st)
+    sample = items[::st].contiguous()
+    ks = D.guess_rank(k, sample.size(0) / I_n)
+    s_smp, _ = ops.score_topk(users, sample, ks)
+    thr = D.threshold_below(s_smp[:, ks - 1].contiguous())
+    del s_smp, sample
+    parts_s, parts_i, bounds = [], [], [D.shard_range(I_n, S, r) for r in range(S)]
+    for lo, hi in bounds:  # each rank's thresholded shard lists (dr_score_topk_seeded)
+        ps, pi = ops.score_topk(users, items[lo:hi], k, item_base=lo, init_thr=thr)
+        parts_s.append(ps)
+        parts_i.append(pi)
+    ms, mi = ops.topk_merge(torch.stack(parts_s), torch.stack(parts_i), k)
+    del parts_s, parts_i
+    # verification + exact fallback (plain per-shard top-k of the failed users)
+    bad = (mi < 0).any(dim=1).nonzero().flatten()
+    assert 0 < bad.numel() < U_n // 50, bad.numel()  # the hot group fails, few others do
+    assert np.isin(hot, bad.cpu().numpy()).mean() > 0.9
+    fs, fi = [], []
+    for lo, hi in bounds:
+        a, b = ops.score_topk(users, items[lo:hi], k, user_ids=bad, item_base=lo)
+        fs.append(a)
+        fi.append(b)
+    ms[bad], mi[bad] = ops.topk_merge(torch.stack(fs), torch.stack(fi), k)
+    rows = np.unique(np.concatenate([rng.choice(U_n, 800, replace=False),
+                                     rng.choice(hot, 200, replace=False)]))
+    _check(users, items, mi, ms, rows, k)
