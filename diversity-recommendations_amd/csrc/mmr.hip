@@ -414,7 +414,10 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
     // radix select bit by bit, both ballots of a step into their own SGPR
     // pairs (hipcc serialises them through VCC). The selection is SALU-bound
     // (the eight waves share the CU's scalar unit); skipping the live values'
-    // common prefix and stopping 8 bits short measured slower (64.3 -> 65.7 ms).
+    // common prefix and stopping 8 bits short measured slower (64.3 -> 65.7 ms),
+    // and so did counting on the VALU (v_bcnt of the ballot halves) on waves
+    // 0-3 or on every wave, which balances the waves but lengthens each step
+    // (65.6 / 66.5 against 64.4 ms).
     static_assert(kPPW + 1 == 9, "the asm below counts against 8");
     auto radix_step = [&](uint32_t p, uint32_t bit) {
       uint64_t ba_, bb_;
