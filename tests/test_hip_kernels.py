@@ -841,6 +841,36 @@ def test_mmr_rerank_invalid_candidates():
         assert (got[u, n_live:] == -1).all()
 
 
+@pytest.mark.parametrize("d,C,lam", [(128, 1000, 0.5), (64, 777, 0.3), (128, 1000, 1.0)])
+def test_mmr_rerank_persistent_prefetch(d, C, lam):
+    """More users than CUs: each workgroup of the persistent grid runs several
+    users, all but its first with ids, scores and tile-0 rows prefetched by
+    LDS-DMA during the previous user. Empty (-1) candidates and an
+    out-of-range id on prefetched users; lam = 1 must equal the top-k by score
+    (ties: lowest position) for every user, lam < 1 every pick a valid greedy
+    step (float64 replay) for users of the prefetched range."""
+    rng = np.random.default_rng(d + C)
+    ni, n, kout = 30000, 700, 100
+    E = oracle.as_bf16_f32((rng.standard_normal((ni, d)) / np.sqrt(d)).astype(np.float32))
+    cand = np.stack([rng.choice(ni, C, replace=False) for _ in range(n)]).astype(np.int32)
+    sc = -np.sort(-rng.random((n, C)), axis=1).astype(np.float32)
+    for u in range(300, n, 37):  # empty slots on prefetched users, some in tile 0
+        cand[u, rng.choice(C, 50, replace=False)] = -1
+    got = ops.mmr_rerank(torch.from_numpy(cand).to(DEV), torch.from_numpy(sc).to(DEV), _bf16(E),
+                         kout, lam).cpu().numpy()
+    if lam == 1.0:
+        for u in range(n):
+            live = cand[u][cand[u] >= 0]
+            assert np.array_equal(got[u], live[:kout]), u
+    else:
+        users = np.concatenate([np.arange(0, 8), rng.choice(np.arange(256, n), 24, replace=False)])
+        assert _mmr_check_positions(got[users], cand[users], sc[users], E, lam, tol=1e-4) == 0
+    bad = cand.copy()
+    bad[500, 3] = ni + 7  # an out-of-range id on a prefetched user: IndexError, as indexing would
+    with pytest.raises(IndexError):
+        ops.mmr_rerank(torch.from_numpy(bad).to(DEV), torch.from_numpy(sc).to(DEV), _bf16(E), kout, lam)
+
+
 # --------------------------------------------------------------------------- catalog histogram
 @pytest.mark.parametrize("dt", [torch.int32, torch.int64])
 def test_catalog_histogram_exact(dt):
