@@ -298,7 +298,10 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
           acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, brow[j][s], acc[j], 0, 0, 0);
       }
       // 1/|pick| per register pair; NaN for rows past the picks, whose
-      // products (NaN) the max ignores: no per-score select
+      // products (NaN) the max ignores: no per-score select. Registers
+      // 8-15 (rows 16-31) are skipped when the pass has at most 16 picks
+      // (the common case: ~15 picks per batch).
+      const bool upper = nrow > 16;
       f32x2 pv2[8];
 #pragma unroll
       for (int gg = 0; gg < 4; ++gg) {
@@ -316,9 +319,16 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
         const f32x2 c2 = {ci, ci};
         float mx = -INFINITY;
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
+        for (int r = 0; r < 8; r += 2) {
           const f32x2 cs = (f32x2{acc[j][r], acc[j][r + 1]} * c2) * pv2[r / 2];
           mx = fmaxf(mx, fmaxf(cs.x, cs.y));
+        }
+        if (upper) {
+#pragma unroll
+          for (int r = 8; r < 16; r += 2) {
+            const f32x2 cs = (f32x2{acc[j][r], acc[j][r + 1]} * c2) * pv2[r / 2];
+            mx = fmaxf(mx, fmaxf(cs.x, cs.y));
+          }
         }
         pen[j] = fmaxf(pen[j], half_swap_max(mx));
       }
@@ -469,14 +479,13 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
     }
     myslot |= (uint32_t)__shfl_xor((int)myslot, 32);  // the other half-wave holds the same rows
     if (lane < kPPW && lane >= nprobe) {
-      // an empty slot: zero row and 1/|e| = 0, so its Gram entries are 0
-      // (finite) and the rounds' max terms stay finite without a select
+      // an empty slot: 1/|e| = 0 (and a zero row, written at staging), so its
+      // Gram entries are 0 (finite) and the rounds' max terms stay finite
+      // without a select
       const int sl = w * kPPW + lane;
       s_pcand[sl] = -1;
       s_pinv[sl] = 0.f;
       s_ppen[sl] = 0.f;
-#pragma unroll
-      for (int c = 0; c < CPR; ++c) s_prow[sl * CPR + c] = uint4{0u, 0u, 0u, 0u};
     }
     // the wave's bound: the best value <= pthr, at its lowest position
     uint64_t wb = 0ull;
@@ -495,6 +504,16 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
     if (lane == 0) s_wbound[w] = wb;
     MG_ADD(kMgSelect, t_sel);
     MG_T0(t_stage);
+    // Staging runs after every wave's fold of the previous batch (each wave
+    // folds before it selects, and the stage barrier below waits for all),
+    // so probe rows, zero rows of empty slots included, are written here and
+    // not during the selection: there is no barrier between a wave's fold and
+    // its next selection.
+    if (lane < kPPW && lane >= nprobe) {
+      const int sl = w * kPPW + lane;
+#pragma unroll
+      for (int c = 0; c < CPR; ++c) s_prow[sl * CPR + c] = uint4{0u, 0u, 0u, 0u};
+    }
 #pragma unroll
     for (int j = 0; j < kTiles; ++j) {
       const int sl = (int)((myslot >> (8 * j)) & 255u) - 1;
@@ -743,7 +762,6 @@ __global__ __launch_bounds__(kThreads) void mmr_pick_kernel(
         if (sl >= 0 && ((picked >> sl) & 1ull)) live &= ~(1u << j);
       }
     }
-    lds_barrier();  // LDS probe state is rewritten by the next batch
     MG_ADD(kMgFold, t_fold);
 #ifdef DR_MMR_DIAG
     dg[kMgBatches] += 1;
