@@ -801,6 +801,10 @@ extern "C" int dr_mmr_rerank(const int32_t* cand_items, const float* cand_scores
   DR_CHECK_ARG(lambda >= 0.f && lambda <= 1.f, "lambda must be in [0, 1]");
   DR_CHECK_ARG(n_items >= 0 && n_items < 0x7fffffffLL, "n_items must be in [0, 2^31)");
   if (n_users == 0) return DR_OK;
+  if (n_items == 0) {  // no row a candidate could name (the kernel reads row 0 for empty slots)
+    dr::set_error("dr_mmr_rerank: empty item table");
+    return DR_EINVAL;
+  }
   DR_CHECK_ARG(cand_items && cand_scores && item_table && out_items, "null pointer");
   hipStream_t s = (hipStream_t)stream;
   // persistent grid: one workgroup per CU (a user's rows take half the

@@ -295,7 +295,9 @@ int dr_catalog_histogram(const void* recs, int rec_dtype, int64_t n_users, int k
  * (item ids in selection order). C <= 1024, k_out <= C, d in {64, 128}.
  * Candidate ids < 0 are empty slots; ids >= n_items are added to *err (int32
  * device counter, may be NULL) and never picked. A user left without live
- * candidates gets -1 for the remaining picks. */
+ * candidates gets -1 for the remaining picks. n_items = 0 is DR_EINVAL.
+ * Launch: one workgroup per CU looping over the users (the next user's
+ * candidates are prefetched while one runs). */
 int dr_mmr_rerank(const int32_t* cand_items, const float* cand_scores, int64_t n_users, int C,
                   const void* item_table, int64_t n_items, int d, int k_out, float lambda,
                   int32_t* out_items, int32_t* err, dr_stream_t stream);

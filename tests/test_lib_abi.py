@@ -87,6 +87,8 @@ def test_argument_errors_without_gpu():
     assert rc == -1 and b"null pointer" in lib.dr_last_error()  # 3 x 1000 > 2048 is accepted
     rc = lib.dr_mmr_rerank(None, None, 4, 2000, None, 10, 128, 10, 0.5, None, None, None)
     assert rc == -1 and b"C must be" in lib.dr_last_error()
+    rc = lib.dr_mmr_rerank(None, None, 4, 100, None, 0, 128, 10, 0.5, None, None, None)
+    assert rc == -1 and b"empty item table" in lib.dr_last_error()
     # empty inputs are a no-op success
     assert lib.dr_gather_dot(None, 0, None, 0, 0, 64, None, None, 0, None, None, None) == 0
     rc = lib.dr_gather_dot(None, -1, None, 0, 0, 64, None, None, 3, None, None, None)
