@@ -251,9 +251,19 @@ def with_measured(roof: dict, dev, key: str) -> dict:
     return roof
 
 
+def same_build(rec: dict) -> bool:
+    """A committed profile record describes the binary this process runs only
+    if it carries the loaded library's build id (the source hash, stamped by
+    tools/pmc_kernels.py / tools/pmc_mfma.py from the profiled run's own bench
+    line); records of other builds, or without an id, are not used."""
+    from divrec import _backend
+
+    return bool(rec.get("build_id")) and rec.get("build_id") == _backend.build_id()
+
+
 def load_traffic(cfg_key: str):
     """HBM bytes per dr_score_topk call from a committed PMC summary
-    (tools/gpu_pmc.sh + tools/pmc_traffic.py) for exactly this config."""
+    (tools/gpu_pmc.sh + tools/pmc_traffic.py) for exactly this config and build."""
     for name in ("pmc_traffic.json", f"pmc_traffic_{cfg_key}.json"):
         path = os.path.join(ROOT, "profiles", name)
         if not os.path.exists(path):
@@ -261,7 +271,7 @@ def load_traffic(cfg_key: str):
         try:
             with open(path) as f:
                 rec = json.load(f)
-            if rec.get("config") == cfg_key:
+            if rec.get("config") == cfg_key and same_build(rec):
                 return rec.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -280,7 +290,7 @@ def pmc_traffic(workload: str, config: str, kernel: str, group: int = 0, per_ste
             rec = json.load(f)
     except (OSError, ValueError):
         return None
-    if rec.get("config") != config:
+    if rec.get("config") != config or not same_build(rec):
         return None
     reps, total, found = int(rec["reps"]), 0.0, False
     for prefix in kernel.split("|"):  # every instantiation of every named kernel
@@ -312,7 +322,7 @@ def pmc_mfma(workload: str, config: str, kernel: str = "score_scan_kernel"):
             rec = json.load(f)
     except (OSError, ValueError):
         return None
-    if rec.get("config") != config:
+    if rec.get("config") != config or not same_build(rec):
         return None
     ks = rec.get("kernels", {})
     k = ks.get(kernel)
@@ -325,7 +335,8 @@ def pmc_mfma(workload: str, config: str, kernel: str = "score_scan_kernel"):
            "mfma_busy_cycles": k["mfma_busy_cycles"], "simd_cycles": k["simd_cycles"],
            "busy_over_flops": k.get("busy_over_expected"),
            "scope": f"every {kernel} dispatch of one call (sample scan, seeded scan, rescan)",
-           "source": f"profiles/pmc_mfma_{workload}.json ({k.get('counters')})"}
+           "source": f"profiles/pmc_mfma_{workload}.json ({k.get('counters')})",
+           "build_id": rec["build_id"]}
     if inst:
         out["main_scan"] = {"kernel": inst, "mfma_busy_frac": ks[inst]["mfma_busy_frac"]}
     return out
@@ -337,6 +348,76 @@ def provenance() -> dict:
     from divrec import _backend
 
     return {"build_id": _backend.build_id()}
+
+
+# --------------------------------------------------------------------------- rank launcher
+def rank_envs(n: int, port: int, base=None) -> list:
+    """The environment of each of n ranks on this node, as torchrun sets it
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*; rendezvous on 127.0.0.1).
+    Pure host logic: no device is touched."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between processes)
+        envs.append(e)
+    return envs
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int, cmd: list, envs: list, poll_s: float = 0.5) -> int:
+    """Run `cmd` once per rank as child processes (one per GPU), from a parent
+    that has made no GPU call (it only waits). Rank 0's stdout is this
+    process's stdout (the one JSON line); the other ranks' stdout goes to
+    stderr. The first rank to fail ends the job: the others are terminated
+    (exact PIDs) and its exit code is returned; 0 when every rank succeeded."""
+    import subprocess
+
+    if torch.cuda.is_initialized():
+        raise RuntimeError("launch_ranks: the parent must not initialise the GPU")
+    procs = [subprocess.Popen(cmd, env=envs[r], stdout=None if r == 0 else sys.stderr)
+             for r in range(n)]
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            failed = [c for c in codes if c not in (None, 0)]
+            if failed:
+                rc = failed[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    finally:
+        live = [p for p in procs if p.poll() is None]
+        for p in live:
+            p.terminate()
+        for p in live:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc
+
+
+def maybe_launch(args) -> int | None:
+    """`--gpus N > 1` outside torchrun (no WORLD_SIZE): start N ranks of this
+    same command, one process per GPU, and return the job's exit code. Under
+    torchrun (WORLD_SIZE set), or at N = 1, None: run in this process."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    return launch_ranks(args.gpus, cmd, rank_envs(args.gpus, free_port()))
 
 
 def time_layout(args, world: int, dev, S: int, record_recs: bool = True):
@@ -362,8 +443,8 @@ def time_layout(args, world: int, dev, S: int, record_recs: bool = True):
         if S > 1 and not args.local_thresholds:
             # shards keep only items above per-user thresholds guessed from a
             # sample of the whole catalog (divrec.distributed.global_thresholds)
-            thr = global_thresholds(users, shard, lo, hi, I_n, k, lay.group)
-            s, i = ops.score_topk(users, shard, k, item_base=lo, init_thr=thr)
+            thr = global_thresholds(users, shard, lo, hi, I_n, k, lay.group)  # [2, n]: tiers
+            s, i = ops.score_topk(users, shard, k, item_base=lo, init_thr=thr[0])
         else:
             s, i = ops.score_topk(users, shard, k, item_base=lo)
         if e:
@@ -409,6 +490,10 @@ def time_layout(args, world: int, dev, S: int, record_recs: bool = True):
 
 def main():
     args = parse()
+    if args.workload in ("catalog", "mmr"):  # the multi-GPU workloads
+        rc = maybe_launch(args)
+        if rc is not None:
+            return rc
     if args.workload == "mmr":
         return mmr_pipeline(args)
     if args.workload != "catalog":
@@ -1145,4 +1230,4 @@ def mmr_pipeline(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

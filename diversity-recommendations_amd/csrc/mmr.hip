@@ -19,6 +19,9 @@
 //     greedy's.
 //   * When no probe beats BOUND the batch ends: one MFMA pass of the batch's
 //     picks against every candidate folds their cosines into the max terms.
+#include <atomic>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -791,6 +794,27 @@ extern "C" int dr_mmr_diag_read(unsigned long long* out, int reset) {
 namespace {
 #endif
 
+// CUs of the current device (cached per device ordinal: a process may drive
+// GPUs of different sizes); DIVREC_SCAN_SLOTS, the planner's test knob, caps
+// the grid so that tests reach many users per workgroup with few users.
+int grid_cus() {
+  static std::atomic<int> cache[64];
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  if (dev >= 0 && dev < 64) n = cache[dev].load(std::memory_order_relaxed);
+  if (n <= 0) {
+    if (dev < 0 || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                       hipSuccess || n <= 0)
+      n = 256;
+    if (dev >= 0 && dev < 64) cache[dev].store(n, std::memory_order_relaxed);
+  }
+  if (const char* e = getenv("DIVREC_SCAN_SLOTS")) {
+    const int v = atoi(e);
+    if (v > 0 && v < n) n = v;
+  }
+  return n;
+}
+
 }  // namespace
 
 extern "C" int dr_mmr_rerank(const int32_t* cand_items, const float* cand_scores, int64_t n_users,
@@ -809,15 +833,7 @@ extern "C" int dr_mmr_rerank(const int32_t* cand_items, const float* cand_scores
   hipStream_t s = (hipStream_t)stream;
   // persistent grid: one workgroup per CU (a user's rows take half the
   // register file), each looping over users and prefetching the next one
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-      cus = n;
-    else
-      cus = 256;
-  }
+  const int cus = grid_cus();
   const dim3 grid((unsigned)(n_users < cus ? n_users : cus));
 #define DR_MMR(DD)                                                                            \
   hipLaunchKernelGGL(mmr_pick_kernel<DD>, grid, dim3(kThreads), 0, s, cand_items, cand_scores,  \

@@ -713,7 +713,9 @@ extern "C" size_t dr_score_topk_workspace(int64_t n_users, int64_t n_items, int 
 // device (planner knobs included), for tests that must prove which plan they
 // ran. out[0..11] = users per workgroup, user blocks, head blocks, tail chunks,
 // chunk items, grid, candidate capacity, sample stride (0 = no guess), sample
-// rows, sample rank ks, main-scan finalize keys of a head user / a tail user.
+// rows, sample rank ks (the safe, second-tier rank), main-scan finalize keys
+// of a head user / a tail user; out[12] (n_out >= 13) the first-tier rank ks1
+// the main scan starts from (= ks for a one-tier guess).
 extern "C" int dr_score_topk_plan(int64_t n_users, int64_t n_items, int dtype, int d, int k,
                                   int64_t* out, int n_out) {
   DR_CHECK_ARG(n_users > 0 && n_items > 0, "sizes must be positive");
@@ -723,17 +725,20 @@ extern "C" int dr_score_topk_plan(int64_t n_users, int64_t n_items, int dtype, i
   DR_CHECK_ARG(out && n_out >= 12, "out must hold 12 values");
   const Layout L = make_layout(n_users, n_items, w, k);
   const Plan& p = L.main;
-  const int64_t v[12] = {p.users_per_wg, p.n_ublocks, p.n_head, p.tail_chunks, p.chunk_items,
+  const int64_t v[13] = {p.users_per_wg, p.n_ublocks, p.n_head, p.tail_chunks, p.chunk_items,
                          p.grid, p.cap, L.g.stride, L.g.S, L.g.ks, head_keys(p, w, k),
-                         tail_keys(p, w, k)};
-  for (int i = 0; i < 12; ++i) out[i] = v[i];
+                         tail_keys(p, w, k), L.g.ks1};
+  const int n = n_out < 13 ? n_out : 13;
+  for (int i = 0; i < n; ++i) out[i] = v[i];
   return DR_OK;
 }
 
 // Users the guessed thresholds failed in the last dr_score_topk call that
 // used this workspace with these arguments: out[0] first tier (rescanned from
 // the safe threshold), out[1] second tier (rescanned from -inf). Host query:
-// a synchronous copy of two device counters (no counters for plain scans: 0).
+// a synchronous copy of the device counters (no counters for plain scans: 0).
+// Whether that call ran two tiers is read from the workspace (the call
+// records it), not re-derived from the current planner knobs.
 extern "C" int dr_score_topk_fail_counts(const void* workspace, int64_t n_users, int64_t n_items,
                                          int dtype, int d, int k, int32_t* out) {
   DR_CHECK_ARG(out, "null out");
@@ -744,10 +749,10 @@ extern "C" int dr_score_topk_fail_counts(const void* workspace, int64_t n_users,
   const Layout L = make_layout(n_users, n_items, w, k);
   if (L.g.S == 0) return DR_OK;
   const char* ws = (const char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
-  DR_CHECK_HIP(hipMemcpy(out, ws + L.off_fcnt(), 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
-  if (L.g.ks1 == L.g.ks) {  // one tier: the first count went straight to the -inf rescan
-    out[1] = out[0];
-  }
+  int32_t c[3] = {0, 0, 0};  // first tier, second tier, "ran two tiers"
+  DR_CHECK_HIP(hipMemcpy(c, ws + L.off_fcnt(), sizeof(c), hipMemcpyDeviceToHost));
+  out[0] = c[0];
+  out[1] = c[2] ? c[1] : c[0];  // one tier: the first count went straight to the -inf rescan
   return DR_OK;
 }
 
@@ -879,8 +884,10 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   float* fthr = two_tier ? (float*)(ws + L.off_fthr()) : nullptr;
   int64_t* frows2 = (int64_t*)(ws + L.off_frows2());
   int64_t* fpos2 = (int64_t*)(ws + L.off_fpos2());
-  int32_t* fcnt = (int32_t*)(ws + L.off_fcnt());  // [0] first-tier failures, [1] second-tier
+  // [0] first-tier failures, [1] second-tier, [2] 1 if this call ran two tiers
+  int32_t* fcnt = (int32_t*)(ws + L.off_fcnt());
   DR_CHECK_HIP(hipMemsetAsync(fcnt, 0, 2 * sizeof(int32_t), s));
+  DR_CHECK_HIP(hipMemsetD32Async((hipDeviceptr_t)(fcnt + 2), two_tier ? 1 : 0, 1, s));
   {
     const int cpr = w / 8;  // 16-B chunks per row
     const int64_t n16 = L.g.S * cpr;

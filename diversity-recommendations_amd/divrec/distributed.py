@@ -87,28 +87,71 @@ def grid_layout(item_shards: int) -> GridLayout:
                       rank // item_shards, group)
 
 
+class Comm:
+    """The collectives of the exchange over one torch.distributed process group
+    (RCCL over xGMI for device tensors; gloo exchanges host copies, for the CPU
+    tests and the one-GPU multi-rank rehearsal). Every rank of the group must
+    call each method in the same order. Any object with the same four members
+    can stand in for it (tests run ranks as threads of one process)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def _staged(self, x: torch.Tensor) -> bool:
+        return x.is_cuda and dist.get_backend(self.group) == "gloo"
+
+    def all_gather_rows(self, x: torch.Tensor, sizes) -> torch.Tensor:
+        """Concatenate every rank's x (rank p holds sizes[p] rows) in rank order."""
+        m = max(max(sizes), 1)
+        staged = self._staged(x)
+        src = x.cpu() if staged else x
+        pad = torch.zeros((m,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        pad[: src.shape[0]] = src
+        outs = [torch.empty_like(pad) for _ in range(self.world)]
+        dist.all_gather(outs, pad, group=self.group)
+        out = torch.cat([o[: sizes[p]] for p, o in enumerate(outs)])
+        return out.to(x.device) if staged else out
+
+    def all_to_all_rows(self, x: torch.Tensor, in_splits, out_splits) -> torch.Tensor:
+        """Rows [sum(in_splits[:p]), +in_splits[p]) of x go to rank p; the
+        result holds out_splits[p] rows from every rank p, in rank order."""
+        staged = self._staged(x)
+        src = x.cpu() if staged else x
+        out = torch.empty((sum(out_splits),) + tuple(src.shape[1:]), dtype=src.dtype,
+                          device=src.device)
+        dist.all_to_all_single(out, src, output_split_sizes=list(out_splits),
+                               input_split_sizes=list(in_splits), group=self.group)
+        return out.to(x.device) if staged else out
+
+    def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
+        staged = self._staged(t)
+        src = t.cpu() if staged else t
+        dist.all_reduce(src, group=self.group)
+        return src.to(t.device) if staged else src
+
+
+def as_comm(group) -> Any:
+    """A Comm for a process group (None = the default group); a Comm-like
+    object is returned as is."""
+    return group if hasattr(group, "all_gather_rows") else Comm(group)
+
+
 def exchange_partials(scores: torch.Tensor, items: torch.Tensor, group=None) -> Partial:
     """all_to_all of per-user partial top-k lists.
 
     Input: this rank's partial lists for ALL n users ([n, k] each).
     Output: [world, n_r, k] scores / items — the partial lists of this rank's
     user slice from every rank (row p = rank p's shard)."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    comm = as_comm(group)
+    world, rank = comm.world, comm.rank
     n, k = scores.shape
     packed = torch.stack([scores.view(torch.int32), items], dim=2).reshape(n, 2 * k).contiguous()
     in_splits = [shard_range(n, world, p)[1] - shard_range(n, world, p)[0] for p in range(world)]
     lo, hi = shard_range(n, world, rank)
     n_r = hi - lo
-    # gloo (CPU tests, the one-GPU multi-rank rehearsal) exchanges host
-    # tensors; RCCL exchanges the device tensors in place over xGMI
-    staged = packed.is_cuda and dist.get_backend(group) == "gloo"
-    src = packed.cpu() if staged else packed
-    out = torch.empty((world * n_r, 2 * k), dtype=torch.int32, device=src.device)
-    dist.all_to_all_single(out, src, output_split_sizes=[n_r] * world,
-                           input_split_sizes=in_splits, group=group)
-    if staged:
-        out = out.to(scores.device)
+    out = comm.all_to_all_rows(packed, in_splits, [n_r] * world)
     out = out.view(world, n_r, k, 2)
     return out[..., 0].contiguous().view(torch.float32), out[..., 1].contiguous()
 
@@ -121,28 +164,33 @@ def global_mean(values: torch.Tensor, group=None) -> torch.Tensor:
     t = torch.stack([values.detach().to(torch.float64).sum(),
                      torch.tensor(float(values.numel()), dtype=torch.float64,
                                   device=values.device)])
-    staged = t.is_cuda and dist.get_backend(group) == "gloo"
-    src = t.cpu() if staged else t
-    dist.all_reduce(src, group=group)
-    return (src[0] / src[1]).to(torch.float32).to(values.device)
+    t = as_comm(group).all_reduce_sum(t)
+    return (t[0] / t[1]).to(torch.float32).to(values.device)
 
 
 # --------------------------------------------------------------------------- global thresholds
 # Each shard of a pure item sharding would otherwise keep its LOCAL top-k: a
 # survivor stream of ~k (1 + ln(I_shard / k)) keys per user on every one of
 # the S shards, where only ~k / S of each shard's items can reach the global
-# top-k. So the ranks first agree on a per-user threshold guessed from a
-# strided sample of the WHOLE catalog (the same rule as dr_score_topk's own
-# guess: stride by catalog length, rank ks = mean + 6 sigma + 3 of the user's
-# top-k inside the sample), and each shard keeps only items above it
-# (dr_score_topk_seeded). The guess is verified after the merge: a user left
-# with fewer than k items is recomputed with plain per-shard top-k lists, so
-# the result is the exact global top-k in every case.
+# top-k. So the ranks first agree on per-user thresholds guessed from a
+# strided sample of the WHOLE catalog, with the single-device guess's rule
+# (csrc/score_topk.hip guess_for): stride by catalog length, mu = k S / I of
+# the user's true top k expected inside the sample, and two tiers:
+#   1. the shards scan from the sample's ks1-th best score, ks1 = mu + 3 sigma
+#      + 1 (about 0.1-0.4 % of users end with fewer than k merged items);
+#   2. those users are rescanned on every shard from their safe threshold, the
+#      sample's ks-th best, ks = mu + 6 sigma + 3 (the one-tier rule of round 2);
+#   3. the users that fail the safe threshold too are rescanned from -inf.
+# Every tier is verified after the merge (a user with fewer than k merged items
+# failed it), so the result is the exact global top-k in every case.
 GUESS_SIGMA = 6.0
-# Users of the last thresholded_exchange call, summed over the ranks of its
-# group, whose guess failed and who were recomputed by the exact fallback
-# (observability for tests and the bench; not used by the path itself).
+GUESS_TIGHT_Z = 3.0
+# Observability of the last thresholded_exchange call, summed over the ranks
+# of its group (tests and the bench; not used by the path itself):
+# LAST_FALLBACK_USERS = users whose first-tier guess failed (recomputed by a
+# later tier); LAST_TIER_FAILURES = (first-tier, second-tier) failure counts.
 LAST_FALLBACK_USERS = 0
+LAST_TIER_FAILURES = (0, 0)
 
 
 def sample_stride(n_items: int, k: int) -> int:
@@ -154,8 +202,18 @@ def sample_stride(n_items: int, k: int) -> int:
 
 
 def guess_rank(k: int, frac: float) -> int:
+    """Safe (second-tier) rank of the guess in the sample: mu + 6 sigma + 3."""
     mu = k * frac
     return min(k, int(math.ceil(mu + GUESS_SIGMA * math.sqrt(mu) + 3.0)))
+
+
+def guess_ranks(k: int, frac: float) -> Tuple[int, int]:
+    """(ks1, ks): the first-tier rank mu + 3 sigma + 1 (at most ks) and the safe
+    rank, as guess_for computes them."""
+    mu = k * frac
+    ks = guess_rank(k, frac)
+    ks1 = max(1, int(math.ceil(mu + GUESS_TIGHT_Z * math.sqrt(mu) + 1.0)))
+    return min(ks1, ks), ks
 
 
 def threshold_below(kth: torch.Tensor) -> torch.Tensor:
@@ -166,17 +224,7 @@ def threshold_below(kth: torch.Tensor) -> torch.Tensor:
 
 
 def _all_gather_rows(x: torch.Tensor, sizes, group) -> torch.Tensor:
-    """Concatenate every rank's x (rank p holds sizes[p] rows) in rank order."""
-    world = len(sizes)
-    m = max(max(sizes), 1)
-    staged = x.is_cuda and dist.get_backend(group) == "gloo"
-    src = x.cpu() if staged else x
-    pad = torch.zeros((m,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
-    pad[: src.shape[0]] = src
-    outs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(outs, pad, group=group)
-    out = torch.cat([o[: sizes[p]] for p, o in enumerate(outs)])
-    return out.to(x.device) if staged else out
+    return as_comm(group).all_gather_rows(x, sizes)
 
 
 def global_thresholds(user_table: torch.Tensor, item_shard: torch.Tensor, lo: int, hi: int,
@@ -185,30 +233,62 @@ def global_thresholds(user_table: torch.Tensor, item_shard: torch.Tensor, lo: in
     """Per-user thresholds for all n users from a sample of the whole catalog:
     every rank contributes its shard's rows at global positions j * stride,
     the samples are all_gathered, each rank ranks ITS merge slice of users
-    against them and the thresholds are all_gathered back. fp32 [n]."""
+    against them and the thresholds are all_gathered back. fp32 [2, n]: row 0
+    the first tier (the shards' scan), row 1 the safe tier (the rescan of the
+    users the first tier failed); -inf where the sample is too short."""
     if local_topk is None:
         from divrec import ops
 
         local_topk = ops.score_topk
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    comm = as_comm(group)
+    world, rank = comm.world, comm.rank
     st = sample_stride(n_items, k)
     j0 = -(-lo // st)  # first global sample position j * st inside [lo, hi)
     rows = item_shard[j0 * st - lo: hi - lo: st]
     # the shards may be any contiguous split: exchange the sample sizes first
     mine = torch.tensor([rows.size(0)], dtype=torch.int64, device=item_shard.device)
-    sizes = [int(c) for c in _all_gather_rows(mine, [1] * world, group).cpu()]
-    sample = _all_gather_rows(rows.contiguous(), sizes, group)
+    sizes = [int(c) for c in comm.all_gather_rows(mine, [1] * world).cpu()]
+    sample = comm.all_gather_rows(rows.contiguous(), sizes)
     n = user_table.size(0) if user_ids is None else user_ids.numel()
     u_lo, u_hi = shard_range(n, world, rank)
-    ks = guess_rank(k, sample.size(0) / n_items) if sample.size(0) else 0
-    thr = torch.full((u_hi - u_lo,), -math.inf, dtype=torch.float32, device=user_table.device)
+    ks1, ks = guess_ranks(k, sample.size(0) / n_items) if sample.size(0) else (0, 0)
+    thr = torch.full((u_hi - u_lo, 2), -math.inf, dtype=torch.float32, device=user_table.device)
     if ks and u_hi > u_lo and sample.size(0) >= ks:
         ids = (user_ids[u_lo:u_hi] if user_ids is not None
                else torch.arange(u_lo, u_hi, device=user_table.device))
         s, _ = local_topk(user_table, sample, ks, user_ids=ids, item_base=0)
-        thr = threshold_below(s[:, ks - 1].contiguous())
+        thr[:, 0] = threshold_below(s[:, ks1 - 1].contiguous())
+        thr[:, 1] = threshold_below(s[:, ks - 1].contiguous())
     usizes = [shard_range(n, world, p)[1] - shard_range(n, world, p)[0] for p in range(world)]
-    return _all_gather_rows(thr, usizes, group)
+    return comm.all_gather_rows(thr, usizes).t().contiguous()
+
+
+def _rescan(comm, user_table, item_shard, lo, k, user_ids, bad, u_lo, cnt, thr_all, merge,
+            local_topk, out_s, out_i):
+    """Recompute the users `bad` (this rank's merge-slice positions; cnt = every
+    rank's count) on every shard from thresholds thr_all[position] (None:
+    -inf), and merge their lists into out_s / out_i. Returns the positions
+    (within bad) of users still left with fewer than k items."""
+    world, rank = comm.world, comm.rank
+    pos = comm.all_gather_rows((bad + u_lo).to(torch.int64), cnt)
+    fids = user_ids[pos] if user_ids is not None else pos
+    init = (torch.full((len(pos),), -math.inf, dtype=torch.float32, device=out_s.device)
+            if thr_all is None else thr_all[pos].contiguous())
+    fs, fi = local_topk(user_table, item_shard, k, user_ids=fids, item_base=lo, init_thr=init)
+    gs = comm.all_gather_rows(fs.contiguous(), [len(pos)] * world).view(world, len(pos), k)
+    gi = comm.all_gather_rows(fi.contiguous(), [len(pos)] * world).view(world, len(pos), k)
+    off = sum(cnt[:rank])
+    if bad.numel():
+        ms, mi = merge(gs[:, off:off + bad.numel()].contiguous(),
+                       gi[:, off:off + bad.numel()].contiguous(), k)
+        out_s[bad], out_i[bad] = ms, mi
+
+
+def _failed(out_i: torch.Tensor, rows: Optional[torch.Tensor], need: int) -> torch.Tensor:
+    """Positions (of `rows`, or of every row) left with fewer than `need` items."""
+    sel = out_i if rows is None else out_i[rows]
+    f = (sel[:, :need] < 0).any(dim=1).nonzero().flatten()
+    return f if rows is None else rows[f]
 
 
 def thresholded_exchange(user_table: torch.Tensor, item_shard: torch.Tensor, lo: int, hi: int,
@@ -218,49 +298,56 @@ def thresholded_exchange(user_table: torch.Tensor, item_shard: torch.Tensor, lo:
                          thr: Optional[torch.Tensor] = None,
                          local: Optional[Partial] = None) -> Partial:
     """Top-k of this rank's merge slice over the sharded catalog with global
-    thresholds (computed here unless given): thresholded shard lists ->
-    all_to_all -> merge -> verification, with an exact fallback for users the
-    guess failed (a user with fewer than min(k, n_items) merged items)."""
+    two-tier thresholds (computed here unless given, [2, n] as from
+    global_thresholds; a [n] tensor is a one-tier guess): first-tier shard
+    lists -> all_to_all -> merge -> verification; the users the first tier
+    failed are rescanned on every shard from their safe thresholds and merged,
+    and those that fail again from -inf, so the lists are exact (a user failed
+    a tier when it is left with fewer than min(k, n_items) merged items)."""
     if local_topk is None or merge is None:
         from divrec import ops
 
         local_topk = local_topk or ops.score_topk
         merge = merge or ops.topk_merge
+    comm = as_comm(group)
     if thr is None:
-        thr = global_thresholds(user_table, item_shard, lo, hi, n_items, k, group, user_ids,
+        thr = global_thresholds(user_table, item_shard, lo, hi, n_items, k, comm, user_ids,
                                 local_topk)
-    if local is None:  # this shard's thresholded lists (the bench passes its timed call's)
+    thr1, thr2 = (thr[0], thr[1]) if thr.dim() == 2 else (thr, None)
+    if local is None:  # this shard's first-tier lists (the bench passes its timed call's)
         local = local_topk(user_table, item_shard, k, user_ids=user_ids, item_base=lo,
-                           init_thr=thr)
+                           init_thr=thr1.contiguous())
     s, i = local
-    ps, pi = exchange_partials(s, i, group)
+    ps, pi = exchange_partials(s, i, comm)
     out_s, out_i = merge(ps, pi, k)
-    # verification: the guess failed for a user left with fewer than k items
     need = min(k, n_items)
-    bad = ((out_i[:, :need] < 0).any(dim=1)).nonzero().flatten()
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    world, rank = comm.world, comm.rank
     n = user_table.size(0) if user_ids is None else user_ids.numel()
     u_lo, _ = shard_range(n, world, rank)
-    mine = torch.tensor([bad.numel()], dtype=torch.int64, device=out_i.device)
-    counts = _all_gather_rows(mine, [1] * world, group)
-    cnt = [int(c) for c in counts.cpu()]
-    global LAST_FALLBACK_USERS
-    LAST_FALLBACK_USERS = sum(cnt)
-    if sum(cnt) == 0:
-        return out_s, out_i
-    # exact fallback: plain per-shard top-k of every failed user, all_gathered
-    pos = _all_gather_rows((bad + u_lo).to(torch.int64), cnt, group)
-    fids = user_ids[pos] if user_ids is not None else pos
-    fs, fi = local_topk(user_table, item_shard, k, user_ids=fids, item_base=lo,
-                        init_thr=torch.full((len(pos),), -math.inf, dtype=torch.float32,
-                                            device=out_s.device))
-    gs = _all_gather_rows(fs.contiguous(), [len(pos)] * world, group).view(world, len(pos), k)
-    gi = _all_gather_rows(fi.contiguous(), [len(pos)] * world, group).view(world, len(pos), k)
-    off = sum(cnt[:rank])
-    if bad.numel():
-        ms, mi = merge(gs[:, off:off + bad.numel()].contiguous(),
-                       gi[:, off:off + bad.numel()].contiguous(), k)
-        out_s[bad], out_i[bad] = ms, mi
+    dev = out_i.device
+
+    def counts(x):
+        c = comm.all_gather_rows(torch.tensor([x.numel()], dtype=torch.int64, device=dev),
+                                 [1] * world)
+        return [int(v) for v in c.cpu()]
+
+    global LAST_FALLBACK_USERS, LAST_TIER_FAILURES
+    bad = _failed(out_i, None, need)
+    cnt = counts(bad)
+    t1, t2 = sum(cnt), 0
+    if t1 and thr2 is not None:  # second tier: the safe thresholds
+        _rescan(comm, user_table, item_shard, lo, k, user_ids, bad, u_lo, cnt, thr2, merge,
+                local_topk, out_s, out_i)
+        bad = _failed(out_i, bad, need)
+        cnt = counts(bad)
+        t2 = sum(cnt)
+    else:
+        t2 = t1
+    if t2:  # last tier: from -inf
+        _rescan(comm, user_table, item_shard, lo, k, user_ids, bad, u_lo, cnt, None, merge,
+                local_topk, out_s, out_i)
+    LAST_FALLBACK_USERS = t1
+    LAST_TIER_FAILURES = (t1, t2)
     return out_s, out_i
 
 
@@ -297,17 +384,18 @@ def sharded_score_topk(
         raise ValueError(f"global_thr needs n_items (the whole catalog's row count) >= "
                          f"item_base + shard rows = {item_base + item_shard.size(0)}, "
                          f"got {n_items}")
-    world = 1 if group is _SOLO else dist.get_world_size(group)
-    rank = 0 if group is _SOLO else dist.get_rank(group)
+    comm = None if group is _SOLO else as_comm(group)
+    world = 1 if comm is None else comm.world
+    rank = 0 if comm is None else comm.rank
     n = user_table.size(0) if user_ids is None else user_ids.numel()
     if global_thr and world > 1:
         out = thresholded_exchange(user_table, item_shard, item_base,
-                                   item_base + item_shard.size(0), n_items, k, group, user_ids,
+                                   item_base + item_shard.size(0), n_items, k, comm, user_ids,
                                    local_topk, merge)
         return out, shard_range(n, world, rank)
     s, i = local_topk(user_table, item_shard, k, user_ids=user_ids, item_base=item_base)
     if world == 1:
         return (s, i), (0, n)
-    ps, pi = exchange_partials(s, i, group)
+    ps, pi = exchange_partials(s, i, comm)
     out = merge(ps, pi, k)
     return out, shard_range(n, world, rank)

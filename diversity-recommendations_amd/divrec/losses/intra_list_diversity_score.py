@@ -112,7 +112,11 @@ class IntraListDiversityScore(RecommendationsAwareLoss):
         sum over itertools.combinations of 0-d tensors of D's dtype, i.e. a
         0-d tensor of that dtype accumulated in order (int 0 for fewer than
         two items). Computed by dr_ild_dense_pair_sum in D's own precision, so
-        the value is bit-identical; returned on D's device."""
+        a float D's value is bit-identical; an integer D is summed exactly in
+        int64 and stored through a double, so it is exact while |sum| < 2^53
+        and, for int32 D, while the sum fits int32 (the reference's int32 sum
+        would wrap there; label matrices of 0/1 never come near either bound).
+        Returned on D's device."""
         recs = user_recommendations.reshape(1, -1)
         if recs.size(1) < 2:
             return 0  # sum() of no pairs

@@ -260,6 +260,18 @@ def pair_wise_train_loop(dataset: PairWiseDataset, model: RankingModel, loss: Pa
                 _backend.host_ids_in_range(pos, I.size(0), "positive item_id")
                 _backend.host_ids_in_range(neg, I.size(0), "negative item_id")
             uid, pid, nid = (t.to(dev, torch.int64, non_blocking=True) for t in (user_id, pos, neg))
+            if not host and uid.numel():
+                # device batches: one min/max reduction read back (one sync)
+                # BEFORE the kernel, so a bad batch raises IndexError with the
+                # weights, the optimizer state and the gradient tables as they
+                # were (the reference's nn.Embedding fails before any backward;
+                # the lazy path's all-zero gradient invariant holds)
+                mm = torch.stack([uid.min(), uid.max(), torch.minimum(pid.min(), nid.min()),
+                                  torch.maximum(pid.max(), nid.max())]).cpu().tolist()
+                if mm[0] < 0 or mm[1] >= U.size(0):
+                    raise IndexError("index out of range in self (user_id)")
+                if mm[2] < 0 or mm[3] >= I.size(0):
+                    raise IndexError("index out of range in self (item_id)")
             if U.grad is None:
                 U.grad = torch.zeros_like(U)
             if I.grad is None:
@@ -270,12 +282,6 @@ def pair_wise_train_loop(dataset: PairWiseDataset, model: RankingModel, loss: Pa
             losses_b, hits = ops.bpr_fwd_bwd(U.data, I.data, uid, pid, nid, 1.0 / B, U.grad, I.grad,
                                              err=epoch_err, check=False)
             loss_value = torch.sum(losses_b, dim=0) / B
-            if not host:
-                # device ids were range-checked by the kernel: read its counter
-                # (one sync) before the optimizer touches the parameters, so a
-                # bad batch raises IndexError with the model as the reference
-                # leaves it (nn.Embedding fails before any update)
-                _backend.raise_if_out_of_range(epoch_err, "pair_wise_train_loop")
             if lazy:  # touched rows only; the kernel zeroes those gradient rows
                 lazy_adam_step(optimizer, {U: torch.unique(uid),
                                            I: torch.unique(torch.cat([pid, nid]))})

@@ -125,7 +125,8 @@ int dr_score_topk(const void* user_table, const int64_t* user_ids, int64_t n_use
  * workgroup, user blocks, head blocks (scanned whole), catalog chunks per tail
  * block (1 = no split), tail chunk length, grid, candidate capacity, sample
  * stride of the guessed threshold (0 = plain scan), sample rows, sample rank ks,
- * finalize keys of a head user, finalize keys of a tail user. n_out >= 12. */
+ * finalize keys of a head user, finalize keys of a tail user; with n_out >= 13,
+ * out[12] = the first-tier rank ks1 <= ks the main scan starts from. n_out >= 12. */
 int dr_score_topk_plan(int64_t n_users, int64_t n_items, int dtype, int d, int k, int64_t* out,
                        int n_out);
 

@@ -618,3 +618,46 @@ def test_device_pairwise_dataset_trains():
     assert all(np.isfinite(h[0]) for h in hist)
     assert hist[-1][0] < hist[0][0]
     assert hist[-1][1][0] > 0.6
+
+
+class _DeviceBatches:
+    """A PairWiseDataset stand-in whose loader yields device batches (as
+    DevicePairWiseDataset does): (user, pos, neg, None, None, None)."""
+
+    def __init__(self, batches):
+        self.batches = batches
+
+    def loader(self, **_):
+        for u, p, n in self.batches:
+            yield u, p, n, None, None, None
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+def test_pair_wise_train_loop_bad_device_batch_leaves_no_trace(sparse):
+    """A device batch with an out-of-range item id raises IndexError before
+    the fused kernel runs: the gradient tables stay as they were,
+    so a caller that catches the error and trains on gets exactly the clean
+    run's weights (dense Adam and the lazy SparseAdam path)."""
+    torch.manual_seed(3)
+    nu, ni, d = 50, 80, 32
+    a = models.MatrixFactorization(nu, ni, d).to(DEV)
+    b = models.MatrixFactorization(nu, ni, d).to(DEV)
+    b.load_state_dict(a.state_dict())
+    mk = (lambda m: torch.optim.SparseAdam(m.parameters(), lr=1e-2)) if sparse else \
+        (lambda m: torch.optim.Adam(m.parameters(), lr=1e-2))
+    oa, ob = mk(a), mk(b)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    good = [tuple(torch.randint(0, n, (64,), generator=g, device=DEV) for n in (nu, ni, ni))
+            for _ in range(2)]
+    bad_n = good[0][2].clone()
+    bad_n[17] = ni + 3
+    loss = losses.LogSigmoidDifferenceLoss()
+    with pytest.raises(IndexError):
+        train.pair_wise_train_loop(_DeviceBatches([(good[0][0], good[0][1], bad_n)]), a, loss, oa)
+    for m in (a,):
+        for p_ in m.parameters():
+            assert p_.grad is None or not p_.grad.any()  # nothing was accumulated
+    train.pair_wise_train_loop(_DeviceBatches(good), a, loss, oa)
+    train.pair_wise_train_loop(_DeviceBatches(good), b, loss, ob)
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa, pb)

@@ -367,3 +367,73 @@ def test_global_thresholds_need_n_items():
         sharded_score_topk(torch.zeros(3, 4), torch.zeros(10, 4), 0, 2, global_thr=True)
     with pytest.raises(ValueError, match="n_items"):
         sharded_score_topk(torch.zeros(3, 4), torch.zeros(10, 4), 5, 2, n_items=12, global_thr=True)
+
+
+def test_two_tier_thresholds_8_thread_ranks():
+    """The default 8-GPU path's two-tier guess (divrec.distributed.
+    thresholded_exchange, the product function) with 8 ranks as threads of
+    this process (tests/thread_comm.py) and the CPU checker top-k. k = 50 at
+    sample stride 32: the first-tier rank in the sample is ks1 = 7, the safe
+    rank ks = 13. Group A's best items are 8 hot rows at sample positions, so
+    its first tier keeps only those 8 (fails) and its safe tier reaches past
+    them (succeeds); group B's 20 hot rows defeat both tiers (the -inf
+    rescan); group C passes the first tier. Lists equal the single-process
+    top-k for every user; the tier counts show who took which tier."""
+    from divrec import distributed as D
+    from divrec.distributed import guess_ranks, sample_stride
+    from thread_comm import ThreadHub
+
+    world, k, d = 8, 50, 16
+    rng = np.random.default_rng(2024)
+    ni = 6007
+    st = sample_stride(ni, k)
+    assert st == 32 and guess_ranks(k, (ni // st + 1) / ni) == (7, 13)
+    I = rng.integers(-3, 4, size=(ni, d)).astype(np.float32)
+    I[:, 14:] = 0.0
+    I[np.arange(8) * st, 15] = 100.0          # group A's hot rows
+    I[np.arange(10, 30) * st, 14] = 100.0     # group B's hot rows
+    U = rng.integers(-3, 4, size=(40, d)).astype(np.float32)
+    U[:, 14:] = 0.0
+    U[:12, 15] = 5.0   # group A
+    U[12:20, 14] = 5.0  # group B
+    bounds = [0, 40, 900, 1000, 2500, 2600, 4100, 5000, ni]  # shard 0 has 40 < k rows
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, return_scores=True)
+
+    def rank_main(comm):
+        lo, hi = bounds[comm.rank], bounds[comm.rank + 1]
+        (s, i), (ulo, uhi) = sharded_score_topk(
+            torch.from_numpy(U), torch.from_numpy(I[lo:hi]), lo, k, group=comm,
+            local_topk=_local_topk_thr, merge=_merge_pad, n_items=ni, global_thr=True)
+        return ulo, uhi, s.numpy(), i.numpy()
+
+    got = ThreadHub(world).run(rank_main)
+    owned = np.zeros(U.shape[0], dtype=int)
+    for r, (ulo, uhi, s, i) in enumerate(got):
+        assert (ulo, uhi) == shard_range(U.shape[0], world, r)
+        assert np.array_equal(i, ref_i[ulo:uhi])
+        assert np.array_equal(s, ref_s[ulo:uhi].astype(np.float32))
+        owned[ulo:uhi] += 1
+    assert (owned == 1).all()
+    t1, t2 = D.LAST_TIER_FAILURES
+    assert t1 >= 20 and 8 <= t2 < t1, D.LAST_TIER_FAILURES
+    assert D.LAST_FALLBACK_USERS == t1
+
+
+def test_thread_comm_matches_exchange_contract():
+    """exchange_partials over the thread comm routes user slices as over gloo
+    (test_exchange_routes_user_slices), so the thread harness is a faithful
+    stand-in for the process group."""
+    from thread_comm import ThreadHub
+
+    world, n, k = 3, 7, 3
+
+    def rank_main(comm):
+        s = torch.full((n, k), float(comm.rank)) + torch.arange(n, dtype=torch.float32)[:, None] / 10
+        i = torch.full((n, k), comm.rank, dtype=torch.int32) * 1000 + torch.arange(n, dtype=torch.int32)[:, None]
+        return exchange_partials(s, i, comm)
+
+    for r, (ps, pi) in enumerate(ThreadHub(world).run(rank_main)):
+        lo, hi = shard_range(n, world, r)
+        assert ps.shape == (world, hi - lo, k)
+        for src in range(world):
+            assert np.array_equal(pi[src, :, 0].numpy(), src * 1000 + np.arange(lo, hi))

@@ -967,3 +967,43 @@ def test_bpr_fwd_bwd_mxm_runs(d):
     sc = keep.sum() / B
     assert np.allclose(gU.cpu().numpy(), rU2 * sc, rtol=1e-4, atol=1e-7)
     assert np.allclose(gI.cpu().numpy(), rI2 * sc, rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("d,C", [(128, 1), (64, 40), (128, 200)])
+def test_mmr_rerank_persistent_prefetch_short_lists(d, C):
+    """Short candidate lists (C < 256: the prefetch pads s_nitem with entry C - 1
+    and tile 0 is only partly live) with k_out == C and more users than CUs:
+    lambda = 1 returns each list in score order, lambda = 0.5 replays as valid
+    greedy steps on prefetched users."""
+    rng = np.random.default_rng(d * 7 + C)
+    ni, n = 5000, 700
+    E = oracle.as_bf16_f32((rng.standard_normal((ni, d)) / np.sqrt(d)).astype(np.float32))
+    cand = np.stack([rng.choice(ni, C, replace=False) for _ in range(n)]).astype(np.int32)
+    sc = -np.sort(-rng.random((n, C)), axis=1).astype(np.float32)
+    ct, st = torch.from_numpy(cand).to(DEV), torch.from_numpy(sc).to(DEV)
+    top = ops.mmr_rerank(ct, st, _bf16(E), C, 1.0).cpu().numpy()
+    assert np.array_equal(top, cand)
+    got = ops.mmr_rerank(ct, st, _bf16(E), C, 0.5).cpu().numpy()
+    users = np.concatenate([np.arange(0, 4), rng.choice(np.arange(256, n), 20, replace=False)])
+    assert _mmr_check_positions(got[users], cand[users], sc[users], E, 0.5, tol=1e-4) == 0
+    assert all(sorted(got[u].tolist()) == sorted(cand[u].tolist()) for u in users)
+
+
+def test_padded_item_table_cached_per_version():
+    """ILD / MMR on a width without a kernel instance (d = 100) pad the item
+    table once per table version: repeated calls reuse the
+    padded copy, an in-place update of the table is seen."""
+    rng = np.random.default_rng(100)
+    ni, d, n, k = 3000, 100, 50, 10
+    E = torch.from_numpy(rng.standard_normal((ni, d)).astype(np.float32)).to(DEV).to(torch.bfloat16)
+    recs = torch.from_numpy(rng.integers(0, ni, (n, k))).to(DEV)
+    a = ops.ild_embedding(recs, E)
+    p1 = ops.pad_columns_cached(E, 128)
+    b = ops.ild_embedding(recs, E)
+    assert ops.pad_columns_cached(E, 128) is p1 and torch.equal(a, b)
+    ref = ops.ild_embedding(recs, ops.pad_columns(E, 128))
+    assert torch.equal(a, ref)
+    E.mul_(2.0)  # version bump: a fresh padded copy (cosine unchanged, dot x4)
+    assert ops.pad_columns_cached(E, 128) is not p1
+    assert torch.allclose(ops.ild_embedding(recs, E, "dot"), 4 * ops.ild_embedding(recs, p1, "dot"),
+                          rtol=1e-5)

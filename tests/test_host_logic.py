@@ -164,14 +164,30 @@ def test_pmc_summaries_feed_bench_traffic(tmp_path):
                             "Counter_Value": v * scale})
     out = tmp_path / "pmc_bpr.json"
     import sys
+
+    from divrec import _backend
+
+    bid = _backend.build_id()
+    # the profiled runs' own bench lines carry the build id that gets stamped
+    (tmp_path / "f.log").write_text("note\n" + json.dumps({"metric": "x", "build_id": bid}) + "\n")
+    (tmp_path / "w.log").write_text(json.dumps({"metric": "x", "build_id": bid}) + "\n")
+    (tmp_path / "old.log").write_text(json.dumps({"metric": "x", "build_id": "0123456789abcdef"}))
     argv = sys.argv
-    sys.argv = ["pmc_kernels.py", str(tmp_path / "f.csv"), str(tmp_path / "w.csv"), "--workload",
-                "bpr", "--reps", "2", "--config", "bpr", "--out", str(out)]
-    try:
-        pk.main()
-    finally:
-        sys.argv = argv
+
+    def run(logs):
+        sys.argv = ["pmc_kernels.py", str(tmp_path / "f.csv"), str(tmp_path / "w.csv"),
+                    "--workload", "bpr", "--reps", "2", "--config", "bpr", "--out", str(out),
+                    "--logs"] + [str(tmp_path / x) for x in logs]
+        try:
+            pk.main()
+        finally:
+            sys.argv = argv
+
+    with pytest.raises(SystemExit):  # runs of two builds: refused
+        run(["f.log", "old.log"])
+    run(["f.log", "w.log"])
     rec = json.load(open(out))
+    assert rec["build_id"] == bid
     assert list(rec["kernels"]) == ["bpr_kernel<4>"]  # the torch kernel is dropped
     hb = rec["kernels"]["bpr_kernel<4>"]["hbm_bytes"]
     assert hb == [1024.0 * (2 * v + 0.5 * v) for v in (10.0, 20.0, 30.0, 40.0)]
@@ -189,6 +205,13 @@ def test_pmc_summaries_feed_bench_traffic(tmp_path):
     assert bench.pmc_traffic("bpr", "bpr", "bpr_kernel", per_step=2) == sum(hb) / 2
     assert bench.pmc_traffic("bpr", "other-config", "bpr_kernel") is None
     assert bench.pmc_traffic("bpr", "bpr", "bpr_kernel", group=2) is None
+    # a record of another build (or without an id) is never used
+    rec["build_id"] = "0123456789abcdef"
+    json.dump(rec, open(tmp_path / "profiles" / "pmc_bpr.json", "w"))
+    assert bench.pmc_traffic("bpr", "bpr", "bpr_kernel", group=0) is None
+    del rec["build_id"]
+    json.dump(rec, open(tmp_path / "profiles" / "pmc_bpr.json", "w"))
+    assert bench.pmc_traffic("bpr", "bpr", "bpr_kernel", group=0) is None
 
 
 def test_global_threshold_helpers():
@@ -205,6 +228,12 @@ def test_global_threshold_helpers():
     assert guess_rank(100, 1 / 32) == 17  # the config-2 guess (ks = 17)
     assert guess_rank(100, 78125 / 10_000_000) == 10
     assert guess_rank(5, 0.9) == 5  # never above k
+    from divrec.distributed import guess_ranks
+
+    assert guess_ranks(100, 1 / 32) == (10, 17)  # config 2: first tier 10, safe 17
+    assert guess_ranks(100, 78125 / 10_000_000) == (5, 10)
+    assert guess_ranks(1000, 1 / 32) == (50, 68)  # config 5's top-1000 scan
+    assert guess_ranks(3, 0.01) == (2, 3)
     s = torch.tensor([1.0, -2.5, 0.0, float("-inf"), float("nan"), 3e-39])
     t = threshold_below(s)
     assert bool((t[:3] < s[:3]).all()) and bool((t[5:] < s[5:]).all())

@@ -205,3 +205,17 @@ def test_distributed_stride_mirrors_the_planner():
             p = ops.score_topk_plan(4096, n, torch.bfloat16, 128, k)
             if p["sample_stride"]:
                 assert sample_stride(n, k) == p["sample_stride"], (n, k)
+
+
+def test_distributed_guess_ranks_mirror_the_planner():
+    """divrec.distributed.guess_ranks (the global two-tier thresholds) must give
+    the single-GPU guess's first-tier and safe ranks (dr_score_topk_plan's
+    first_tier_rank and sample_rank) for the same sample fraction."""
+    from divrec.distributed import guess_ranks
+
+    for n in (1 << 18, 1_000_000, 1_250_000, 5_000_000, 10_000_000):
+        for k in (10, 50, 100, 1000):
+            p = ops.score_topk_plan(4096, n, torch.bfloat16, 128, k)
+            if p["sample_stride"]:
+                assert guess_ranks(k, p["sample_rows"] / n) == (p["first_tier_rank"],
+                                                                p["sample_rank"]), (n, k)

@@ -290,17 +290,19 @@ def test_config2_plan_1m_x_1m_d64_exact():
 
 def test_configs3_eight_way_item_shards_full_size():
     """BASELINE configs[3] as bench.py --gpus 8 lays it out: the 10M-item
-    catalog row-sharded 8 ways (1.25M rows per rank), every rank scoring all
-    1M users against its shard from the global sample thresholds
-    (divrec.distributed.global_thresholds' rule: the whole catalog's rows at
-    the single-device stride, rank ks = guess_rank, threshold_below), then the
-    merge of the 8 thresholded partial lists and the exact fallback for users
-    the guess failed — thresholded_exchange's steps on one GPU, all eight
-    ranks' kernel calls in sequence (RCCL transport aside). Integer tables,
-    hot rows at sample positions for a user group (their guess fails and they
-    go through the fallback). Checked: the merged lists of ~1000 users, hot
-    ones included, against the exact top-k of the whole catalog."""
+    catalog row-sharded 8 ways (1.25M rows per rank), run by the product
+    function itself — divrec.distributed.sharded_score_topk(global_thr=True):
+    global two-tier sample thresholds, dr_score_topk_seeded per shard, the
+    all_to_all of partial lists, dr_topk_merge, verification and the tier-2 /
+    -inf rescans — with the eight ranks as threads of this process on cuda:0
+    (tests/thread_comm.py stands in for RCCL). Integer tables; 7 hot rows (+3)
+    at global sample positions defeat group A's first tier (rank 5) but not
+    its safe tier (rank 10); 12 hot rows (-3) defeat both tiers of the
+    non-positive group B (the -inf rescan). Checked: the tier counts, and the
+    merged lists of ~1000 users, both groups included, against the exact top-k
+    of the whole catalog."""
     from divrec import distributed as D
+    from thread_comm import ThreadHub
 
     U_n, I_n, d, k, S = 1_000_000, 10_000_000, 128, 100, 8
     rng = np.random.default_rng(8)
@@ -308,33 +310,81 @@ def test_configs3_eight_way_item_shards_full_size():
     items = _int_table_dev(I_n, d, 32)
     st = D.sample_stride(I_n, k)
     assert st == ops.score_topk_plan(U_n, I_n, torch.bfloat16, d, k)["sample_stride"] == 128
-    items[torch.arange(12, device=DEV) * st] = 3.0  # hot rows inside the sample, on shard 0
-    hot = np.unique(rng.choice(U_n, 2000, replace=False))
+    assert D.guess_ranks(k, (I_n // st) / I_n) == (5, 10)
+    items[torch.arange(7, device=DEV) * st] = 3.0            # group A's hot rows (shard 0)
+    items[torch.arange(20, 32, device=DEV) * st] = -3.0      # group B's hot rows
+    grp = rng.choice(U_n, 2000, replace=False)
+    ga, gb = np.sort(grp[:1000]), np.sort(grp[1000:])
+    ga_t, gb_t = torch.as_tensor(ga, device=DEV), torch.as_tensor(gb, device=DEV)
+    users[ga_t] = users[ga_t].abs()
+    users[gb_t] = -users[gb_t].abs()
+    torch.cuda.synchronize()
+
+    def rank_main(comm):
+        lo, hi = D.shard_range(I_n, S, comm.rank)
+        (s, i), (ulo, uhi) = D.sharded_score_topk(users, items[lo:hi], lo, k, group=comm,
+                                                  n_items=I_n, global_thr=True)
+        return ulo, uhi, s, i
+
+    got = ThreadHub(S).run(rank_main)
+    torch.cuda.synchronize()
+    t1, t2 = D.LAST_TIER_FAILURES
+    assert t1 >= 2000 - 20 and 1000 - 10 <= t2 < t1 - 900, D.LAST_TIER_FAILURES
+    assert [(a, b) for a, b, _, _ in got] == [D.shard_range(U_n, S, r) for r in range(S)]
+    ms = torch.cat([g[2] for g in got])
+    mi = torch.cat([g[3] for g in got])
+    del got
+    rows = np.unique(np.concatenate([rng.choice(U_n, 700, replace=False),
+                                     rng.choice(ga, 150, replace=False),
+                                     rng.choice(gb, 150, replace=False)]))
+    _check(users, items, mi, ms, rows, k)
+
+
+def test_config5_plan_1m_x_10m_k1000_then_mmr():
+    """BASELINE configs[4] at one GPU, the calls bench.py --workload mmr times:
+    the top-1000 scan of 1M users over the 10M-item catalog (d = 128; stride-32
+    two-tier guess, CAP 2048, long-list flush) and the MMR re-rank of those
+    1000 candidates to 100 on the persistent grid. Integer tables; 60 hot rows
+    at sample positions are the best items of a non-negative user group, whose
+    first-tier (rank 50) and safe (rank 68) thresholds both fall inside the hot
+    scores: the group goes through every tier down to the -inf rescan. Checked:
+    ~600 users from head, split-tail and last blocks plus 100 of the hot group
+    against the exact top-1000 (lists and scores); then MMR over all 1M lists:
+    lambda = 1 equals each list's first 100 for every user, and at lambda = 0.5
+    ~200 users spread over the grid (first users of their CU, prefetched users,
+    the last round) replay as valid greedy steps in float64."""
+    U_n, I_n, d, k = 1_000_000, 10_000_000, 128, 1000
+    plan = ops.score_topk_plan(U_n, I_n, torch.bfloat16, d, k)
+    assert (plan["sample_stride"], plan["cap"], plan["user_blocks"]) == (32, 2048, 977), plan
+    assert (plan["first_tier_rank"], plan["sample_rank"]) == (50, 68), plan
+    rng = np.random.default_rng(5005)
+    users = _int_table_dev(U_n, d, 41)
+    items = _int_table_dev(I_n, d, 42)
+    items[torch.arange(60, device=DEV) * 32] = 3.0
+    hot = np.unique(rng.choice(U_n, 1000, replace=False))
     hot_t = torch.as_tensor(hot, device=DEV)
     users[hot_t] = users[hot_t].abs()
-    # global thresholds from the whole catalog's sample (every rank's rows at j * st)
-    sample = items[::st].contiguous()
-    ks = D.guess_rank(k, sample.size(0) / I_n)
-    s_smp, _ = ops.score_topk(users, sample, ks)
-    thr = D.threshold_below(s_smp[:, ks - 1].contiguous())
-    del s_smp, sample
-    parts_s, parts_i, bounds = [], [], [D.shard_range(I_n, S, r) for r in range(S)]
-    for lo, hi in bounds:  # each rank's thresholded shard lists (dr_score_topk_seeded)
-        ps, pi = ops.score_topk(users, items[lo:hi], k, item_base=lo, init_thr=thr)
-        parts_s.append(ps)
-        parts_i.append(pi)
-    ms, mi = ops.topk_merge(torch.stack(parts_s), torch.stack(parts_i), k)
-    del parts_s, parts_i
-    # verification + exact fallback (plain per-shard top-k of the failed users)
-    bad = (mi < 0).any(dim=1).nonzero().flatten()
-    assert 0 < bad.numel() < U_n // 50, bad.numel()  # the hot group fails, few others do
-    assert np.isin(hot, bad.cpu().numpy()).mean() > 0.9
-    fs, fi = [], []
-    for lo, hi in bounds:
-        a, b = ops.score_topk(users, items[lo:hi], k, user_ids=bad, item_base=lo)
-        fs.append(a)
-        fi.append(b)
-    ms[bad], mi[bad] = ops.topk_merge(torch.stack(fs), torch.stack(fi), k)
-    rows = np.unique(np.concatenate([rng.choice(U_n, 800, replace=False),
-                                     rng.choice(hot, 200, replace=False)]))
-    _check(users, items, mi, ms, rows, k)
+    st = {}
+    s, it = ops.score_topk(users, items, k, stats=st)
+    t1, t2 = st["guess_failures"]
+    assert t1 >= len(hot) and t2 >= len(hot) - 10, st
+    rows = _sample_rows(rng, plan, U_n, 250, 200, 100)
+    _check(users, items, it, s, rows, k)
+    _check(users, items, it, s, rng.choice(hot, 100, replace=False), k)
+    # MMR on the persistent grid over every user's real top-1000 list
+    top = ops.mmr_rerank(it, s, items, 100, 1.0)
+    assert torch.equal(top, it[:, :100])
+    picks = ops.mmr_rerank(it, s, items, 100, 0.5).cpu().numpy()
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    sel = np.unique(np.concatenate([np.arange(0, 40), rng.choice(np.arange(cus, U_n - cus), 120,
+                                                                  replace=False),
+                                    np.arange(U_n - 40, U_n)]))
+    sel_t = torch.as_tensor(sel, device=DEV)
+    cand, sc = it[sel_t].cpu().numpy(), s[sel_t].cpu().numpy()
+    # the replay needs only the selected users' candidate rows: ids remapped
+    uniq = np.unique(cand)
+    E = items[torch.as_tensor(uniq, device=DEV, dtype=torch.int64)].float().cpu().numpy()
+    remap = lambda x: np.where(x >= 0, np.searchsorted(uniq, x), -1)  # noqa: E731
+    from test_hip_kernels import _mmr_check_positions
+
+    assert _mmr_check_positions(remap(picks[sel]), remap(cand), sc, E, 0.5, tol=1e-4) == 0

@@ -28,5 +28,5 @@ for w in $WL; do
   timeout -s KILL $lim rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmck/$w/fetch -o fetch -- python3 $R/bench.py $args --no-cpu-baseline > $R/gpurun_out/pmck/$w.fetch.log 2>&1
   timeout -s KILL $lim rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmck/$w/write -o write -- python3 $R/bench.py $args --no-cpu-baseline > $R/gpurun_out/pmck/$w.write.log 2>&1
   cd $R
-  python3 tools/pmc_kernels.py gpurun_out/pmck/$w/fetch/fetch_counter_collection.csv gpurun_out/pmck/$w/write/write_counter_collection.csv --workload $w --reps $reps --config $cfg --out gpurun_out/pmck/pmc_$w.json > gpurun_out/pmck/$w.summary.txt
+  python3 tools/pmc_kernels.py gpurun_out/pmck/$w/fetch/fetch_counter_collection.csv gpurun_out/pmck/$w/write/write_counter_collection.csv --workload $w --reps $reps --config $cfg --logs gpurun_out/pmck/$w.fetch.log gpurun_out/pmck/$w.write.log gpurun_out/pmck/$w.trace.log --out gpurun_out/pmck/pmc_$w.json > gpurun_out/pmck/$w.summary.txt
 done

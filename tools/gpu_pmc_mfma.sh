@@ -31,5 +31,5 @@ for r in csv.DictReader(open(sys.argv[1])):
 print(tot)
 PY
 )
-  python3 tools/pmc_mfma.py gpurun_out/pmcm/$w/mfma/mfma_counter_collection.csv --workload $w --reps 1 --config $cfg --flops $flops --kernel-ms $kms --out gpurun_out/pmcm/pmc_mfma_$w.json > gpurun_out/pmcm/$w.summary.txt
+  python3 tools/pmc_mfma.py gpurun_out/pmcm/$w/mfma/mfma_counter_collection.csv --workload $w --reps 1 --config $cfg --flops $flops --kernel-ms $kms --logs gpurun_out/pmcm/$w.mfma.log gpurun_out/pmcm/$w.trace.log --out gpurun_out/pmcm/pmc_mfma_$w.json > gpurun_out/pmcm/$w.summary.txt
 done

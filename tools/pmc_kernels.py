@@ -14,6 +14,11 @@ access widths are uncalibrated (the adam_kernel line, whose traffic is known
 exactly, is the in-run calibration). `reps` = warmup + steps of the pass: the
 dispatches of a kernel come in groups of `reps` (one group per workload
 phase), which bench.py averages into `roofline.traffic`.
+
+Provenance: --logs names the profiled runs' own bench output; the build id
+(libdivrec_hip's source hash) their JSON lines print is stamped into the
+record, and bench.py uses a record only when that id equals the id of the
+library it has loaded. Runs of different builds are refused.
 """
 import argparse
 import csv
@@ -61,6 +66,24 @@ def per_dispatch(path, counter):
     return out
 
 
+def build_id_of(logs):
+    """The one build id printed by the bench lines of these logs (error if
+    none, or if the runs loaded different builds)."""
+    ids = set()
+    for path in logs:
+        with open(path) as f:
+            for line in f:
+                line = line.strip()
+                if line.startswith("{") and '"build_id"' in line:
+                    try:
+                        ids.add(json.loads(line)["build_id"])
+                    except (ValueError, KeyError):
+                        pass
+    if len(ids) != 1:
+        raise SystemExit(f"expected one build id in {logs}, found {sorted(ids)}")
+    return ids.pop()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_csv")
@@ -69,7 +92,10 @@ def main():
     ap.add_argument("--reps", type=int, required=True, help="warmup + steps of the PMC passes")
     ap.add_argument("--config", default="")
     ap.add_argument("--out", default="")
+    ap.add_argument("--logs", nargs="+", required=True,
+                    help="bench output of the profiled runs (their build id is stamped)")
     args = ap.parse_args()
+    bid = build_id_of(args.logs)
     f = per_dispatch(args.fetch_csv, "FETCH_SIZE")
     w = per_dispatch(args.write_csv, "WRITE_SIZE")
     kernels = {}
@@ -80,7 +106,7 @@ def main():
                          "write_bytes": wr,
                          "hbm_bytes": [2.0 * a + b for a, b in zip(fr, wr)]}
     rec = {"workload": args.workload, "config": args.config, "reps": args.reps,
-           "kernels": kernels,
+           "build_id": bid, "kernels": kernels,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of the "
                      "same command; per dispatch; FETCH_SIZE x2 (gfx950 wide-read correction), "
                      "KB x 1024"}

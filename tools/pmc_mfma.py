@@ -26,7 +26,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from pmc_kernels import OURS, short_name  # noqa: E402
+from pmc_kernels import OURS, build_id_of, short_name  # noqa: E402
 
 N_SIMDS = 1024
 COUNTERS = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE")
@@ -42,7 +42,10 @@ def main():
     ap.add_argument("--flops-kernel", default="score_scan_kernel")
     ap.add_argument("--kernel-ms", type=float, default=0.0)
     ap.add_argument("--out", default="")
+    ap.add_argument("--logs", nargs="+", required=True,
+                    help="bench output of the profiled runs (their build id is stamped)")
     args = ap.parse_args()
+    bid = build_id_of(args.logs)
     per = {}  # (dispatch, name) -> {counter: value}
     with open(args.csv) as f:
         for r in csv.DictReader(f):
@@ -77,7 +80,7 @@ def main():
         if name == args.flops_kernel and args.kernel_ms:
             rec["clock_ghz"] = grbm / 8.0 / (args.kernel_ms * 1e-3) / 1e9
         out[name] = rec
-    res = {"workload": args.workload, "config": args.config, "reps": args.reps,
+    res = {"workload": args.workload, "config": args.config, "reps": args.reps, "build_id": bid,
            "method": "rocprofv3 --pmc " + " ".join(COUNTERS) + " (one pass); "
                      "mfma_busy_frac = MFMA_BUSY / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)",
            "kernels": out}
