@@ -88,6 +88,14 @@ enum {
 #ifndef DR_APIPE
 #define DR_APIPE 1  // A fragments read two k-steps ahead
 #endif
+#ifndef DR_BALANCE
+// SIMD-pair balance: the two waves of a SIMD (w, w ^ 4) publish their tile
+// index in LDS once per tile; the one behind its partner (ties: waves 4-7)
+// raises its issue priority. Without it the arbiter's age order lets waves
+// 0-3 run ahead within a stage and wait at its barrier while their partners
+// finish alone, their epilogues no longer hidden under MFMAs.
+#define DR_BALANCE 0
+#endif
 #ifndef DR_FLUSH_GAP
 #define DR_FLUSH_GAP 96  // new keys a buffer takes past k + kSlack before compaction
 #endif
@@ -641,8 +649,9 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
   // user tile: the area must hold a whole wave's worth of blocks
   static_assert(!STAGED || SB >= 64, "staging area smaller than a wave");
   constexpr int WAVE_BYTES = UPW * 4 + 256 * 4 + SB * (64 + 12);
-  static_assert(RING_BYTES + kWaves * WAVE_BYTES <= 163840, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char smem[RING_BYTES + kWaves * WAVE_BYTES];
+  constexpr int PROG_BYTES = DR_BALANCE ? kWaves * 4 : 0;  // per-wave tile index (DR_BALANCE)
+  static_assert(RING_BYTES + kWaves * WAVE_BYTES + PROG_BYTES <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[RING_BYTES + kWaves * WAVE_BYTES + PROG_BYTES];
 
   // A buffer is compacted once it holds more than flush_at keys; a stage adds
   // at most MARGIN keys per user, so flush_at + MARGIN <= CAP. A small gap
@@ -762,13 +771,41 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
       u32x4 af[KS];
       af[0] = ds_read_b128_asm(tb + a_off(0));
       if constexpr (KS > 1) af[1] = ds_read_b128_asm(tb + a_off(1));
+#if DR_BALANCE
+      // this wave's tile index out, its partner's in; issued with the last
+      // A-fragment read, retired by the final lgkmcnt(0) below (which names pt)
+      constexpr bool kProg = decltype(GI)::value == 0;
+      uint32_t pt = 0u;
+#endif
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         if (s + 1 < KS) lds_wait1(af[s]);
+#if DR_BALANCE
+        else if (kProg)
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[s]), "+v"(pt) : : "memory");
+#endif
         else lds_wait0(af[s]);
         if (s + 2 < KS) af[s + 2] = ds_read_b128_asm(tb + a_off(s + 2));
+#if DR_BALANCE
+        if (kProg && s == (KS > 2 ? KS - 3 : 0)) {
+          const uint32_t pa = lds_ring + RING_BYTES + kWaves * WAVE_BYTES;
+          const uint32_t mine = pa + 4u * (uint32_t)wave, other = pa + 4u * (uint32_t)(wave ^ 4);
+          asm volatile("ds_write_b32 %0, %1" : : "v"(mine), "v"((uint32_t)t) : "memory");
+          asm volatile("ds_read_b32 %0, %1" : "=v"(pt) : "v"(other) : "memory");
+        }
+#endif
         kstep_mma<F32, NG>(af[s], bfr, g0, s, acc);
       }
+#if DR_BALANCE
+      if constexpr (kProg) {
+        // behind the partner (ties: waves 4-7, the ones age order disfavours):
+        // priority for this tile's epilogue and the next tile's MFMA issue
+        const int ptu = __builtin_amdgcn_readfirstlane((int)pt);
+        const bool behind = ptu > t || (ptu == t && wave >= 4);
+        if (behind) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+#endif
 #else
       constexpr int HALF = KS >= 4 ? KS / 2 : KS;
 #pragma unroll

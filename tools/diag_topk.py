@@ -14,7 +14,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "diversity-recommendations_amd")
-os.environ["DIVREC_HIP_LIB"] = os.path.join(PKG, "divrec", "_lib", "libdivrec_hip_diag.so")
+_tag = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--lib=")), "diag")
+os.environ["DIVREC_HIP_LIB"] = os.path.join(PKG, "divrec", "_lib", f"libdivrec_hip_{_tag}.so")
 sys.path.insert(0, PKG)
 sys.path.insert(0, ROOT)
 
@@ -32,6 +33,7 @@ def main():
     ap.add_argument("--items", type=int, default=10_000_000)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--lib", default="diag", help="diag library tag (libdivrec_hip_<tag>.so)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(1)
@@ -75,6 +77,12 @@ def main():
     res["cycles_per_tile"] = cyc / max(1, res["n_tiles"])
     # in-kernel shader clock: s_memtime cycles / s_memrealtime ticks (100 MHz)
     res["clock_ghz"] = cyc / max(1.0, res["realtime_100mhz"]) * 0.1
+    # per SIMD-pair half: waves 0-3 (older, favoured by the arbiter's age
+    # order) against their partners 4-7 on the same SIMDs
+    for half, name in ((range(0, 4), "waves0_3"), (range(4, 8), "waves4_7")):
+        sel = [r for i, r in enumerate(recs) if i % 8 in half]
+        t = [sum(r[i] for r in sel) / max(1, len(sel)) for i in range(len(SLOTS))]
+        res[name] = {nm: round(t[i] / max(1.0, t[0]), 4) for i, nm in enumerate(SLOTS[1:8], 1)}
     print(json.dumps(res))
 
 
