@@ -585,6 +585,16 @@ struct TopkArgs {
   // blocks' chunk-0 rows, bounded by buf_blocks user blocks of buffer rows.
   int dev_split;
   int64_t buf_blocks;
+  // Sample scans of the guessed thresholds (the GMAX instantiation): a lane keeps
+  // only the MAX of its 16 scores of a user tile (one key per 16-row group of a
+  // tile) instead of every score above the threshold. The k-th best group max
+  // is a lower bound of the k-th best score (the best k groups' maxima are k
+  // distinct items), so the guessed threshold stays a valid lower bound — it
+  // only drops below the exact sample rank when two of the best k sample
+  // items share a group (~k^2 / (2 S / 16) of users) — while the survivor
+  // stream of a scan from -inf shrinks up to 16-fold. Keys name the group
+  // (tile row base + 4h), not an item: only their scores are read.
+  int gmax;
   // Fallback rescan only: the user count lives on the device (n_users and
   // n_ublocks above are its upper bounds), and pos_map[p] is the caller's
   // position of list entry p (its exclusion row). NULL otherwise.
@@ -624,8 +634,9 @@ __host__ __device__ inline DevSplit dev_split_plan(int64_t nb, int64_t grid, int
   return d;
 }
 
-template <int W, int CAP, bool SEEDED, bool F32>
+template <int W, int CAP, bool SEEDED, bool F32, bool GMAX = false>
 __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkArgs a) {
+  static_assert(!(GMAX && SEEDED), "group-max scans are the (unseeded) sample scans");
   constexpr int D = W;  // geometry is by row bytes: an fp32 row of d is a bf16 row of 2d
   using G = TileGeom<D>;
   constexpr int NU_T = nut_for(D);
@@ -1108,13 +1119,46 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
       DG_ADD(kDgEnqueue, t_e);
       DG_CNT(kDgNEnqueue);
     };
+    // Group-max enqueue (GMAX sample scans): one key per hitting lane, the max
+    // of its 16 scores. It is the whole epilogue of such a scan (the max is
+    // its hot test too). A partial last tile (rows past the slice end repeat
+    // the last row) is skipped: leaving sample rows out only lowers the
+    // sample's order statistics, so the guess stays a lower bound.
+    auto enqueue_gmax = [&](int t, f32x16 (&acc)[NG], auto GI) {
+      constexpr int g0 = decltype(GI)::value * NG;
+      DG_T0(t_e);
+      const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
+      if (i_end - tile0 < kTileItems) return;
+#pragma unroll
+      for (int ut = 0; ut < NG; ++ut) {
+        float m = acc[ut][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) m = fmaxf(m, acc[ut][r]);
+        const bool hit = m > thr[g0 + ut];
+        if (__ballot(hit) == 0ull) continue;
+        if (hit) {
+          const int slot = (g0 + ut) * 32 + col;
+          const uint32_t pos = atomicAdd(&ucnt[slot], 1u);
+          const uint32_t gkey = (uint32_t)(a.item_base + tile0) + 4u * (uint32_t)h;
+          if (pos < (uint32_t)CAP) st64(cbase + (size_t)slot * CAP + pos, dr::make_key(m, gkey));
+        }
+        vmc += 1;  // the store above issued once (some lane had a key)
+      }
+      DG_ADD(kDgEnqueue, t_e);
+      DG_CNT(kDgNEnqueue);
+    };
     auto epilogue = [&](int t, f32x16 (&acc)[NG], auto GI) {
+      // the stage-end work runs after the last group of the tile
+      constexpr bool last_group = decltype(GI)::value == NGRP - 1;
+      if constexpr (GMAX) {  // sample scan: group maxima only
+        enqueue_gmax(t, acc, GI);
+        if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) check_compact(flush_at, a.slack);
+        return;
+      }
       DG_T0(t_h);
       uint32_t hit_bits = any_hits(acc, GI);
       DG_ADD(kDgHits, t_h);
       hit_bits = __builtin_amdgcn_readfirstlane(hit_bits);  // ballots: uniform
-      // the stage-end work runs after the last group of the tile
-      constexpr bool last_group = decltype(GI)::value == NGRP - 1;
       if constexpr (STAGED) {
         if (hit_bits != 0u) stage_hits(t, acc, hit_bits, GI);
         // end of a stage: resolve the staged blocks, compact full buffers
@@ -1256,7 +1300,14 @@ bool launch_scan_widths(const Plan& p, const TopkArgs& a, int w, bool seeded, hi
     done = true;
 #define DR_SCAN(CC, SD) \
   hipLaunchKernelGGL((score_scan_kernel<WW, CC, SD, F32>), dim3(p.grid), dim3(kThreads), 0, s, a)
-    if (p.cap == 512) {
+#define DR_SCAN_GMAX(CC) \
+  hipLaunchKernelGGL((score_scan_kernel<WW, CC, false, F32, true>), dim3(p.grid), dim3(kThreads), \
+                     0, s, a)
+    if (a.gmax && !seeded) {  // sample scans (ks <= ~70 keys: CAP 512, or 1024 at narrow rows)
+      if (p.cap == 512) DR_SCAN_GMAX(512);
+      else if (p.cap == 1024) DR_SCAN_GMAX(1024);
+      else done = false;
+    } else if (p.cap == 512) {
       if (seeded) DR_SCAN(512, true); else DR_SCAN(512, false);
     } else if (p.cap == 1024) {
       if (seeded) DR_SCAN(1024, true); else DR_SCAN(1024, false);
@@ -1266,6 +1317,7 @@ bool launch_scan_widths(const Plan& p, const TopkArgs& a, int w, bool seeded, hi
       done = false;
     }
 #undef DR_SCAN
+#undef DR_SCAN_GMAX
   };
   (one(IC<Ws>{}), ...);
   return done;

@@ -387,6 +387,9 @@ constexpr int kMaxTailChunks = 16;
 #ifndef DR_SAMPLE_GAP
 #define DR_SAMPLE_GAP 96
 #endif
+#ifndef DR_SAMPLE_GMAX
+#define DR_SAMPLE_GMAX 1  // sample scans keep group maxima (TopkArgs::gmax); 0: every survivor
+#endif
 constexpr int kSampleSlack = DR_SAMPLE_SLACK;
 constexpr int kSampleGap = DR_SAMPLE_GAP;
 // The finalize of a split-tail user sorts every chunk's end-compacted keys
@@ -562,7 +565,10 @@ Guess guess_for(int64_t n_items, int k, bool split_tail) {
   g.stride = kGuessStride;
   while (k < DR_GUESS_LONG_K && g.stride < 128 && n_items / (2 * g.stride) >= 65536) g.stride *= 2;
   if (const char* e = getenv("DIVREC_GUESS_STRIDE")) g.stride = atoi(e) > 1 ? atoi(e) : g.stride;  // A/B knob
-  g.S = n_items / g.stride;
+  // a whole number of 32-row tiles: the sample is stored tile-transposed
+  // (sample_rows_kernel), and rows left out only lower the sample's order
+  // statistics, so the guess stays a lower bound
+  g.S = n_items / g.stride / kTileItems * kTileItems;
   const double mu = (double)k * (double)g.S / (double)n_items;
   int ks = (int)ceil(mu + DR_GUESS_SIGMA * sqrt(mu) + 3.0);
   g.ks = ks < k ? ks : k;
@@ -632,14 +638,21 @@ Layout make_layout(int64_t n_users, int64_t n_items, int w, int k) {
   return L;
 }
 
-// Sample rows: out[i] = I[i * stride], 16 B per thread.
+// Sample rows, tile-transposed: the S = 32 T sample rows j * stride (j < S)
+// are stored so that sample j = q T + r sits in row q of tile r, i.e. output
+// row p = 32 r + q. A 16-row lane group of a tile (the GMAX sample scan keeps
+// one max per group) then holds samples T apart — catalog rows T * stride
+// apart — so items that cluster by id (e.g. ids ordered by popularity) fall
+// into different groups. 16 B per thread.
 __global__ __launch_bounds__(256) void sample_rows_kernel(const uint4* __restrict__ I,
                                                           int64_t stride, int64_t S, int cpr,
                                                           uint4* __restrict__ out) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= S * cpr) return;
-  const int64_t r = t / cpr, c = t % cpr;
-  out[t] = I[r * stride * cpr + c];
+  const int64_t p = t / cpr, c = t % cpr;
+  const int64_t T = S / kTileItems;
+  const int64_t j = (p % kTileItems) * T + p / kTileItems;
+  out[t] = I[j * stride * cpr + c];
 }
 
 
@@ -909,6 +922,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   as.end_keep = ps.end_keep;
   as.slack = ps.slack;
   as.gap = ps.gap;
+  as.gmax = DR_SAMPLE_GMAX;
   DR_SCAN_OR_FAIL(ps, as, false)
   DR_CHECK_LAUNCH();
   {
