@@ -799,10 +799,15 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
         if (s + 2 < KS) af[s + 2] = ds_read_b128_asm(tb + a_off(s + 2));
 #if DR_BALANCE
         if (kProg && s == (KS > 2 ? KS - 3 : 0)) {
-          const uint32_t pa = lds_ring + RING_BYTES + kWaves * WAVE_BYTES;
-          const uint32_t mine = pa + 4u * (uint32_t)wave, other = pa + 4u * (uint32_t)(wave ^ 4);
-          asm volatile("ds_write_b32 %0, %1" : : "v"(mine), "v"((uint32_t)t) : "memory");
-          asm volatile("ds_read_b32 %0, %1" : "=v"(pt) : "v"(other) : "memory");
+          // slots: wave w at pair base + 16 (w >> 2); one address register,
+          // the halves' offsets as immediates under a uniform branch
+          const uint32_t pb = lds_ring + RING_BYTES + kWaves * WAVE_BYTES + 4u * (uint32_t)(wave & 3);
+          if (wave < 4)
+            asm volatile("ds_write_b32 %1, %2\n\tds_read_b32 %0, %1 offset:16"
+                         : "=v"(pt) : "v"(pb), "v"((uint32_t)t) : "memory");
+          else
+            asm volatile("ds_write_b32 %1, %2 offset:16\n\tds_read_b32 %0, %1"
+                         : "=v"(pt) : "v"(pb), "v"((uint32_t)t) : "memory");
         }
 #endif
         kstep_mma<F32, NG>(af[s], bfr, g0, s, acc);
