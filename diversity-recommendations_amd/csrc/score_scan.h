@@ -818,7 +818,13 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
         // priority for this tile's epilogue and the next tile's MFMA issue
         const int ptu = __builtin_amdgcn_readfirstlane((int)pt);
         const bool behind = ptu > t || (ptu == t && wave >= 4);
+#if DR_BALANCE == 2  // A/B: the wave AHEAD gets the priority (the hypothesis' control)
+        if (!behind) __builtin_amdgcn_s_setprio(2);
+#elif DR_BALANCE == 3  // A/B: a one-step priority difference
+        if (behind) __builtin_amdgcn_s_setprio(1);
+#else
         if (behind) __builtin_amdgcn_s_setprio(2);
+#endif
         else __builtin_amdgcn_s_setprio(0);
       }
 #endif

@@ -14,6 +14,6 @@ timeout -k 10 600 python3 -u -m pytest tests/test_real_plans.py tests/test_hip_k
 timeout -k 10 300 python3 -u tools/diag_topk.py --lib=diag --users 262144 --items 10000000 --dim 128 --k 100 > $O/diag.json 2> $O/diag.err
 timeout -k 10 300 python3 -u tools/diag_topk.py --lib=baldiag --users 262144 --items 10000000 --dim 128 --k 100 > $O/baldiag.json 2> $O/baldiag.err
 timeout -k 10 400 python3 -u tools/variant_bench.py --libs product,nogmax,bal,product@DIVREC_GUESS_STRIDE=16,product@DIVREC_GUESS_STRIDE=8 --users 1000000 --items 1000000 --dim 64 --rounds 3 > $O/ab_cfg2.json 2> $O/ab_cfg2.err
-timeout -k 10 400 python3 -u tools/variant_bench.py --libs product,nogmax,bal --users 1000000 --items 10000000 --dim 128 --rounds 2 > $O/ab_10m.json 2> $O/ab_10m.err
+timeout -k 10 400 python3 -u tools/variant_bench.py --libs product,nogmax,bal,balinv,bal1 --users 1000000 --items 10000000 --dim 128 --rounds 2 > $O/ab_10m.json 2> $O/ab_10m.err
 timeout -k 10 400 python3 -u tools/variant_bench.py --libs product,nogmax,bal --users 262144 --items 10000000 --dim 128 --k 1000 --rounds 2 > $O/ab_k1000.json 2> $O/ab_k1000.err
 timeout -k 10 400 python3 -u tools/variant_bench.py --libs product,bal --users 1000000 --items 1250000 --dim 128 --rounds 3 > $O/ab_1m25.json 2> $O/ab_1m25.err
