@@ -1132,6 +1132,143 @@ extern "C" int dr_score_topk_seeded(const void* user_table, const int64_t* user_
   return DR_OK;
 }
 
+// ------------------------------------------------------------------ sample thresholds
+// dr_sample_thresholds: the guess of dr_score_topk on a caller-gathered sample
+// (divrec.distributed.global_thresholds): tile-transposed copy of the whole
+// tiles of the sample, the GMAX sample scan (k = ks), thresholds at ranks ks1
+// and ks. Workspace: [cand | cnt | transposed sample].
+struct SampleThrLayout {
+  Plan p;
+  int64_t S = 0;
+  size_t cand = 0, cnt = 0, samp = 0;
+  size_t total() const { return cand + cnt + samp; }
+};
+
+SampleThrLayout sample_thr_layout(int64_t n_users, int64_t n_sample, int w, int ks) {
+  SampleThrLayout L;
+  L.S = n_sample / kTileItems * kTileItems;
+  if (L.S == 0) return L;
+  L.p = make_plan(n_users, L.S, w, ks, false);
+  L.p.slack = kSampleSlack;
+  L.p.gap = kSampleGap;
+  L.cand = al256(L.p.cand_bytes);
+  L.cnt = al256(L.p.cnt_bytes);
+  L.samp = al256((size_t)L.S * w * 2);
+  return L;
+}
+
+// out row p = 32 r + q <- sample row q T + r (T = S / 32), 16 B per thread
+__global__ __launch_bounds__(256) void transpose_tiles_kernel(const uint4* __restrict__ in,
+                                                              int64_t S, int cpr,
+                                                              uint4* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= S * cpr) return;
+  const int64_t p = t / cpr, c = t % cpr;
+  const int64_t T = S / kTileItems;
+  out[t] = in[((p % kTileItems) * T + p / kTileItems) * cpr + c];
+}
+
+__global__ __launch_bounds__(256) void fill_f32_kernel(float* __restrict__ a, float* __restrict__ b,
+                                                       int64_t n, float v) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < n) {
+    a[t] = v;
+    b[t] = v;
+  }
+}
+
+extern "C" size_t dr_sample_thresholds_workspace(int64_t n_users, int64_t n_sample, int dtype,
+                                                 int d, int ks) {
+  if (n_users <= 0 || n_sample < 0 || ks <= 0 || ks > 256) return 0;
+  const int w = width_for(dtype, d);
+  if (w < 0 || cap_for(w, ks) < 0) return 0;
+  return sample_thr_layout(n_users, n_sample, w, ks).total() + 256;
+}
+
+extern "C" int dr_sample_thresholds(const void* user_table, const int64_t* user_ids,
+                                    int64_t n_users, const void* sample_rows, int64_t n_sample,
+                                    int dtype, int d, int ks1, int ks, float* thr1, float* thr2,
+                                    void* workspace, size_t workspace_bytes, dr_stream_t stream) {
+  DR_CHECK_ARG(n_users >= 0 && n_sample >= 0, "negative size");
+  DR_CHECK_ARG(ks >= 1 && ks <= 256 && ks1 >= 1 && ks1 <= ks, "need 1 <= ks1 <= ks <= 256");
+  DR_CHECK_ARG(dtype == DR_BF16 || dtype == DR_F32, "tables must be DR_BF16 or DR_F32");
+  const int w = width_for(dtype, d);
+  DR_CHECK_ARG(w > 0 && cap_for(w, ks) > 0, "unsupported dtype / d");
+  if (n_users == 0) return DR_OK;
+  DR_CHECK_ARG(user_table && thr1 && thr2, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const SampleThrLayout L = sample_thr_layout(n_users, n_sample, w, ks);
+  if (L.S == 0) {  // no whole tile of sample rows: no guess
+    hipLaunchKernelGGL(fill_f32_kernel, dim3((unsigned)dr::ceil_div(n_users, 256)), dim3(256), 0, s,
+                       thr1, thr2, n_users, -INFINITY);
+    DR_CHECK_LAUNCH();
+    return DR_OK;
+  }
+  DR_CHECK_ARG(sample_rows, "null sample_rows");
+  char* ws = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  if (!workspace || (size_t)(ws - (char*)workspace) + L.total() > workspace_bytes) {
+    dr::set_error("dr_sample_thresholds: workspace too small (need " +
+                  std::to_string(L.total() + 256) + " bytes)");
+    return DR_EWORKSPACE;
+  }
+  char* samp = ws + L.cand + L.cnt;
+  {
+    const int cpr = w / 8;
+    hipLaunchKernelGGL(transpose_tiles_kernel, dim3((unsigned)dr::ceil_div(L.S * cpr, 256)),
+                       dim3(256), 0, s, (const uint4*)sample_rows, L.S, cpr, (uint4*)samp);
+    DR_CHECK_LAUNCH();
+  }
+  const Plan& p = L.p;
+  TopkArgs a{};
+  a.U = (const char*)user_table;
+  a.user_ids = user_ids;
+  a.n_users = n_users;
+  a.n_users_pad = p.n_users_pad;
+  a.I = samp;
+  a.n_items = L.S;
+  a.k = ks;
+  a.n_ublocks = p.n_ublocks;
+  a.n_head = p.n_head;
+  a.tail_chunks = p.tail_chunks;
+  a.chunk_items = p.chunk_items;
+  a.end_keep = p.end_keep;
+  a.slack = p.slack;
+  a.gap = p.gap;
+  a.gmax = 1;
+  a.cand = (uint64_t*)ws;
+  a.cnt = (int32_t*)(ws + L.cand);
+  if (!launch_scan(p, a, dtype, w, false, s)) {
+    dr::set_error("dr_sample_thresholds: internal plan error (no scan instance)");
+    return DR_EUNSUPPORTED;
+  }
+  DR_CHECK_LAUNCH();
+  const BufMap sm = buf_map(p);
+  const int64_t sh = p.head_users() < n_users ? p.head_users() : n_users;
+  int64_t T0 = 0, T1 = sh;
+  for (int part = 0; part < 2; ++part) {
+    if (T1 > T0) {
+      const int P = p_for(part == 0 ? head_keys(p, w, ks) : tail_keys(p, w, ks));
+#define DR_STHR(PP)                                                                              \
+  hipLaunchKernelGGL((topk_threshold_kernel<PP>), dim3((unsigned)dr::ceil_div(T1 - T0, 4)),      \
+                     dim3(256), 0, s, a.cand, a.cnt, sm, p.cap, T0, T1, n_users, ks, ks1, thr1, thr2)
+      switch (P) {
+        case 4: DR_STHR(4); break;
+        case 8: DR_STHR(8); break;
+        case 16: DR_STHR(16); break;
+        case 32: DR_STHR(32); break;
+        default:
+          dr::set_error("dr_sample_thresholds: internal plan error (candidate sort)");
+          return DR_EUNSUPPORTED;
+      }
+#undef DR_STHR
+      DR_CHECK_LAUNCH();
+    }
+    T0 = sh;
+    T1 = n_users;
+  }
+  return DR_OK;
+}
+
 extern "C" int dr_topk_merge(const float* in_scores, const int32_t* in_items, int parts,
                              int64_t n_users, int k_in, int k_out, float* out_scores,
                              int32_t* out_items, dr_stream_t stream) {

@@ -55,6 +55,9 @@ SIGNATURES = {
         _i32,
         [_p, _p, _i64, _p, _i64, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p, _sz, _p],
     ),
+    "dr_sample_thresholds_workspace": (_sz, [_i64, _i64, _i32, _i32, _i32]),
+    "dr_sample_thresholds": (_i32, [_p, _p, _i64, _p, _i64, _i32, _i32, _i32, _i32, _p, _p, _p,
+                                    _sz, _p]),
     "dr_topk_merge": (_i32, [_p, _p, _i32, _i64, _i32, _i32, _p, _p, _p]),
     "dr_ild_dense": (_i32, [_p, _i32, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),
     "dr_ild_dense_pair_sum": (_i32, [_p, _i32, _i64, _i32, _p, _i32, _i64, _p, _p, _p]),

@@ -235,11 +235,18 @@ def global_thresholds(user_table: torch.Tensor, item_shard: torch.Tensor, lo: in
     the samples are all_gathered, each rank ranks ITS merge slice of users
     against them and the thresholds are all_gathered back. fp32 [2, n]: row 0
     the first tier (the shards' scan), row 1 the safe tier (the rescan of the
-    users the first tier failed); -inf where the sample is too short."""
+    users the first tier failed); -inf where the sample is too short.
+
+    On the HIP kernels (no ``local_topk`` given) the ranking is
+    dr_sample_thresholds: the single-GPU guess's group-max sample scan, so the
+    thresholds are lower bounds of the sample ranks. An injected
+    ``local_topk`` (CPU tests) ranks the exact sample top-ks instead."""
+    sample_thr = None
     if local_topk is None:
         from divrec import ops
 
         local_topk = ops.score_topk
+        sample_thr = ops.sample_thresholds
     comm = as_comm(group)
     world, rank = comm.world, comm.rank
     st = sample_stride(n_items, k)
@@ -256,9 +263,12 @@ def global_thresholds(user_table: torch.Tensor, item_shard: torch.Tensor, lo: in
     if ks and u_hi > u_lo and sample.size(0) >= ks:
         ids = (user_ids[u_lo:u_hi] if user_ids is not None
                else torch.arange(u_lo, u_hi, device=user_table.device))
-        s, _ = local_topk(user_table, sample, ks, user_ids=ids, item_base=0)
-        thr[:, 0] = threshold_below(s[:, ks1 - 1].contiguous())
-        thr[:, 1] = threshold_below(s[:, ks - 1].contiguous())
+        if sample_thr is not None:
+            thr = sample_thr(user_table, sample, ks1, ks, user_ids=ids).t().contiguous()
+        else:
+            s, _ = local_topk(user_table, sample, ks, user_ids=ids, item_base=0)
+            thr[:, 0] = threshold_below(s[:, ks1 - 1].contiguous())
+            thr[:, 1] = threshold_below(s[:, ks - 1].contiguous())
     usizes = [shard_range(n, world, p)[1] - shard_range(n, world, p)[0] for p in range(world)]
     return comm.all_gather_rows(thr, usizes).t().contiguous()
 

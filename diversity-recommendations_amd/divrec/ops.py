@@ -250,6 +250,44 @@ def score_topk_plan(n_users: int, n_items: int, dtype: torch.dtype, d: int, k: i
     return dict(zip(PLAN_FIELDS, (int(x) for x in out)))
 
 
+def sample_thresholds(user_table: torch.Tensor, sample_rows: torch.Tensor, ks1: int, ks: int,
+                      user_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The guessed thresholds of the item-sharded top-k (dr_sample_thresholds):
+    ``sample_rows`` are the whole catalog's rows at the guess stride; returns
+    fp32 [2, n]: strictly below each user's ks1-th (row 0, first tier) and
+    ks-th (row 1, safe tier) best group-max score of the sample (the
+    dr_score_topk guess's group-max sample scan; -inf when there are fewer)."""
+    dev = B.require_device(user_table, sample_rows, user_ids)
+    _need(user_table.dtype == sample_rows.dtype and user_table.dtype in SCORE_WIDTHS,
+          "user table and sample rows must both be bf16 or both fp32")
+    _need(user_table.dim() == 2 and sample_rows.dim() == 2 and
+          sample_rows.size(1) == user_table.size(1), "2-D tables of one width")
+    _need(1 <= ks1 <= ks <= 256, "need 1 <= ks1 <= ks <= 256")
+    _contig(user_table, "user_table")
+    w = score_width(user_table.dtype, user_table.size(1))
+    user_table = pad_columns(user_table, w)
+    sample_rows = pad_columns(sample_rows.contiguous(), w)
+    if user_ids is not None:
+        _need(user_ids.dtype == torch.int64 and user_ids.dim() == 1, "user_ids must be 1-D int64")
+        user_ids = user_ids.contiguous()
+        n = user_ids.numel()
+    else:
+        n = user_table.size(0)
+    out = torch.empty((2, n), dtype=torch.float32, device=dev)
+    if n == 0:
+        return out
+    L = B.lib()
+    dt = B.dtype_code(user_table.dtype)
+    ws_bytes = L.dr_sample_thresholds_workspace(n, sample_rows.size(0), dt, w, int(ks))
+    ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=dev)
+    rc = L.dr_sample_thresholds(user_table.data_ptr(), B.ptr(user_ids), n,
+                                sample_rows.data_ptr(), sample_rows.size(0), dt, w, int(ks1),
+                                int(ks), out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(),
+                                ws.numel(), B.stream(dev))
+    B.check(rc, "dr_sample_thresholds")
+    return out
+
+
 def topk_merge(
     scores: torch.Tensor, items: torch.Tensor, k_out: Optional[int] = None
 ) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -138,6 +138,23 @@ int dr_score_topk_plan(int64_t n_users, int64_t n_items, int dtype, int d, int k
 int dr_score_topk_fail_counts(const void* workspace, int64_t n_users, int64_t n_items, int dtype,
                               int d, int k, int32_t* out);
 
+/* The guessed thresholds of the item-sharded multi-GPU top-k, computed like
+ * dr_score_topk's own guess: sample_rows [n_sample, d] (dtype as the user
+ * table) are the whole catalog's rows at the guess stride, gathered from every
+ * shard; the whole 32-row tiles of them (n_sample rounded down) are scanned by
+ * the group-max sample scan, and thr1[u] / thr2[u] (fp32 [n_users], device)
+ * are set strictly below the ks1-th / ks-th best group-max score of user u
+ * (-inf when there are fewer): lower bounds of the user's ks1-th / ks-th best
+ * sample score, the first-tier and safe thresholds of
+ * divrec.distributed.thresholded_exchange (replaces nothing in the reference:
+ * the scale-out of divrec/train/utils.py:53-77). 1 <= ks1 <= ks <= 256.
+ * Workspace of dr_sample_thresholds_workspace(...) bytes. */
+size_t dr_sample_thresholds_workspace(int64_t n_users, int64_t n_sample, int dtype, int d, int ks);
+int dr_sample_thresholds(const void* user_table, const int64_t* user_ids, int64_t n_users,
+                         const void* sample_rows, int64_t n_sample, int dtype, int d, int ks1,
+                         int ks, float* thr1, float* thr2, void* workspace, size_t workspace_bytes,
+                         dr_stream_t stream);
+
 /* dr_score_topk with caller-given per-user thresholds: the top-k (same order)
  * of the items whose score is STRICTLY above init_thr[u]; slots past the last
  * such item hold item -1 and score -inf. init_thr fp32 [n_users] (-inf = plain

@@ -1007,3 +1007,42 @@ def test_padded_item_table_cached_per_version():
     assert ops.pad_columns_cached(E, 128) is not p1
     assert torch.allclose(ops.ild_embedding(recs, E, "dot"), 4 * ops.ild_embedding(recs, p1, "dot"),
                           rtol=1e-5)
+
+
+@pytest.mark.parametrize("d,n_sample,ks1,ks,ids", [(128, 78125, 5, 10, False), (64, 31250, 10, 17, True),
+                                                   (128, 70, 1, 3, False), (64, 5000, 50, 68, True),
+                                                   (32, 31, 1, 2, False)])
+def test_sample_thresholds_group_max(d, n_sample, ks1, ks, ids):
+    """dr_sample_thresholds (the item-sharded path's guess): the whole 32-row
+    tiles of the sample, tile-transposed (sample q T + r -> row q of tile r),
+    one max per 16-row lane group (rows 4h + 8i + j of a tile), thresholds
+    strictly below each user's ks1-th / ks-th best group max (-inf with fewer
+    groups). Integer tables: every score exact, so the thresholds must equal a
+    torch restatement bit for bit, and never exceed the exact sample ranks."""
+    from divrec.distributed import threshold_below
+
+    rng = np.random.default_rng(d + n_sample + ks)
+    nu = 2500
+    U = _int_table(rng, nu, d)
+    Sm = _int_table(rng, n_sample, d)
+    uids = rng.permutation(nu)[:1800].astype(np.int64) if ids else None
+    Ub, Sb = _bf16(U), _bf16(Sm)
+    out = ops.sample_thresholds(Ub, Sb, ks1, ks,
+                                user_ids=None if uids is None else torch.from_numpy(uids).to(DEV))
+    Uq = U if uids is None else U[uids]
+    Sp = n_sample // 32 * 32
+    ref = torch.full((2, Uq.shape[0]), -float("inf"))
+    if Sp:
+        T = Sp // 32
+        idx = np.array([(p % 32) * T + p // 32 for p in range(Sp)])
+        sc = torch.from_numpy(Uq.astype(np.float64) @ Sm[idx].astype(np.float64).T)
+        sc = sc.view(-1, T, 4, 2, 4)  # tile, i, h, j (row = 4h + 8i + j)
+        gm = sc.amax(dim=(2, 4)).reshape(sc.shape[0], 2 * T)
+        top = torch.sort(gm, dim=1, descending=True).values
+        for row, kk in ((0, ks1), (1, ks)):
+            if 2 * T >= kk:
+                ref[row] = threshold_below(top[:, kk - 1].float())
+        exact = torch.sort(torch.from_numpy(Uq.astype(np.float64) @ Sm.astype(np.float64).T), dim=1,
+                           descending=True).values
+        assert (ref[1].double() <= exact[:, ks - 1]).all()  # a lower bound of the exact rank
+    assert torch.equal(out.cpu(), ref)
