@@ -10,7 +10,7 @@ set -e
 export TMPDIR=/tmp
 O=gpurun_out/ab1
 mkdir -p $O
-timeout -k 10 600 python3 -u -m pytest tests/test_real_plans.py tests/test_hip_kernels.py -m gpu -x -q --timeout 300 --timeout-method thread -k "score_topk or plan or tier or rescan or stride" > $O/tests.log 2>&1
+timeout -k 10 600 python3 -u -m pytest tests/test_real_plans.py tests/test_hip_kernels.py -m gpu -x -q --timeout 300 --timeout-method thread -k "score_topk or plan or tier or rescan or stride or thresholds" > $O/tests.log 2>&1
 timeout -k 10 300 python3 -u tools/diag_topk.py --lib=diag --users 262144 --items 10000000 --dim 128 --k 100 > $O/diag.json 2> $O/diag.err
 timeout -k 10 300 python3 -u tools/diag_topk.py --lib=baldiag --users 262144 --items 10000000 --dim 128 --k 100 > $O/baldiag.json 2> $O/baldiag.err
 timeout -k 10 400 python3 -u tools/variant_bench.py --libs product,nogmax,bal,product@DIVREC_GUESS_STRIDE=16,product@DIVREC_GUESS_STRIDE=8 --users 1000000 --items 1000000 --dim 64 --rounds 3 > $O/ab_cfg2.json 2> $O/ab_cfg2.err
