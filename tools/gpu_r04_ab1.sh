@@ -17,3 +17,4 @@ timeout -k 10 400 python3 -u tools/variant_bench.py --libs product,nogmax,bal,pr
 timeout -k 10 400 python3 -u tools/variant_bench.py --libs product,nogmax,bal,balinv,bal1 --users 1000000 --items 10000000 --dim 128 --rounds 2 > $O/ab_10m.json 2> $O/ab_10m.err
 timeout -k 10 400 python3 -u tools/variant_bench.py --libs product,nogmax,bal --users 262144 --items 10000000 --dim 128 --k 1000 --rounds 2 > $O/ab_k1000.json 2> $O/ab_k1000.err
 timeout -k 10 400 python3 -u tools/variant_bench.py --libs product,bal --users 1000000 --items 1250000 --dim 128 --rounds 3 > $O/ab_1m25.json 2> $O/ab_1m25.err
+timeout -k 10 300 python3 -u tools/shard_thr_ab.py --shards 8 > $O/shard8.json 2> $O/shard8.err

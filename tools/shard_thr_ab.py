@@ -3,6 +3,9 @@
 with per-user thresholds guessed from a sample of the whole catalog
 (dr_score_topk_seeded, divrec.distributed's global thresholds), plus the
 threshold step's own cost at the merge-slice size it has under S ranks.
+Round 4: the shard scan from the first-tier thresholds of dr_sample_thresholds
+beside the round-2 one-tier (6-sigma) rule. Which users the merge sends to the
+second tier is not observable on one shard; the kept-item counts are reported.
 
     python tools/shard_thr_ab.py [--shards 8] [--users 1000000] [--items 10000000]
 """
@@ -20,7 +23,8 @@ import torch  # noqa: E402
 
 from bench import gen_table  # noqa: E402
 from divrec import ops  # noqa: E402
-from divrec.distributed import guess_rank, sample_stride, shard_range, threshold_below  # noqa: E402
+from divrec.distributed import (guess_rank, guess_ranks, sample_stride, shard_range,  # noqa: E402
+                               threshold_below)
 
 
 def timed(fn, reps=3):
@@ -61,11 +65,24 @@ def main():
     t_seed, (gs, gi) = timed(lambda: ops.score_topk(users, shard, a.k, item_base=lo, init_thr=thr))
     # every global top-k item of this shard is in the thresholded list
     kept = (gi >= 0).sum(1).float()
+    # round 4: two tiers from the group-max sample scan (dr_sample_thresholds)
+    ks1, ks2 = guess_ranks(a.k, sample.size(0) / a.items)
+    t_thr2, _ = timed(lambda: ops.sample_thresholds(users, sample, ks1, ks2, user_ids=ids))
+    thr2 = ops.sample_thresholds(users, sample, ks1, ks2)
+    t_tier1, (ts, ti) = timed(lambda: ops.score_topk(users, shard, a.k, item_base=lo,
+                                                     init_thr=thr2[0].contiguous()))
+    kept1 = (ti >= 0).sum(1).float()
     print(json.dumps({
         "shards": a.shards, "users": a.users, "items": a.items, "shard_items": hi - lo,
         "sample_stride": st, "ks": ks, "local_topk_ms": t_local, "thresholded_ms": t_seed,
         "threshold_step_ms_per_rank": t_thr, "mean_items_kept_per_user": float(kept.mean()),
-        "gain": t_local / (t_seed + t_thr) - 1.0}), flush=True)
+        "gain": t_local / (t_seed + t_thr) - 1.0,
+        "two_tier": {"ks1": ks1, "ks": ks2, "tier1_scan_ms": t_tier1,
+                     "sample_thresholds_ms_per_rank": t_thr2,
+                     "mean_items_kept_per_user": float(kept1.mean()),
+                     "gain_vs_local": t_local / (t_tier1 + t_thr2) - 1.0,
+                     "gain_vs_one_tier": (t_seed + t_thr) / (t_tier1 + t_thr2) - 1.0}}),
+          flush=True)
 
 
 if __name__ == "__main__":
