@@ -88,14 +88,6 @@ enum {
 #ifndef DR_APIPE
 #define DR_APIPE 1  // A fragments read two k-steps ahead
 #endif
-#ifndef DR_BALANCE
-// SIMD-pair balance: the two waves of a SIMD (w, w ^ 4) publish their tile
-// index in LDS once per tile; the one behind its partner (ties: waves 4-7)
-// raises its issue priority. Without it the arbiter's age order lets waves
-// 0-3 run ahead within a stage and wait at its barrier while their partners
-// finish alone, their epilogues no longer hidden under MFMAs.
-#define DR_BALANCE 0
-#endif
 #ifndef DR_FLUSH_GAP
 #define DR_FLUSH_GAP 96  // new keys a buffer takes past k + kSlack before compaction
 #endif
@@ -660,9 +652,8 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
   // user tile: the area must hold a whole wave's worth of blocks
   static_assert(!STAGED || SB >= 64, "staging area smaller than a wave");
   constexpr int WAVE_BYTES = UPW * 4 + 256 * 4 + SB * (64 + 12);
-  constexpr int PROG_BYTES = DR_BALANCE ? kWaves * 4 : 0;  // per-wave tile index (DR_BALANCE)
-  static_assert(RING_BYTES + kWaves * WAVE_BYTES + PROG_BYTES <= 163840, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char smem[RING_BYTES + kWaves * WAVE_BYTES + PROG_BYTES];
+  static_assert(RING_BYTES + kWaves * WAVE_BYTES <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[RING_BYTES + kWaves * WAVE_BYTES];
 
   // A buffer is compacted once it holds more than flush_at keys; a stage adds
   // at most MARGIN keys per user, so flush_at + MARGIN <= CAP. A small gap
@@ -782,52 +773,13 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
       u32x4 af[KS];
       af[0] = ds_read_b128_asm(tb + a_off(0));
       if constexpr (KS > 1) af[1] = ds_read_b128_asm(tb + a_off(1));
-#if DR_BALANCE
-      // this wave's tile index out, its partner's in; issued with the last
-      // A-fragment read, retired by the final lgkmcnt(0) below (which names pt)
-      constexpr bool kProg = decltype(GI)::value == 0;
-      uint32_t pt = 0u;
-#endif
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         if (s + 1 < KS) lds_wait1(af[s]);
-#if DR_BALANCE
-        else if (kProg)
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[s]), "+v"(pt) : : "memory");
-#endif
         else lds_wait0(af[s]);
         if (s + 2 < KS) af[s + 2] = ds_read_b128_asm(tb + a_off(s + 2));
-#if DR_BALANCE
-        if (kProg && s == (KS > 2 ? KS - 3 : 0)) {
-          // slots: wave w at pair base + 16 (w >> 2); one address register,
-          // the halves' offsets as immediates under a uniform branch
-          const uint32_t pb = lds_ring + RING_BYTES + kWaves * WAVE_BYTES + 4u * (uint32_t)(wave & 3);
-          if (wave < 4)
-            asm volatile("ds_write_b32 %1, %2\n\tds_read_b32 %0, %1 offset:16"
-                         : "=v"(pt) : "v"(pb), "v"((uint32_t)t) : "memory");
-          else
-            asm volatile("ds_write_b32 %1, %2 offset:16\n\tds_read_b32 %0, %1"
-                         : "=v"(pt) : "v"(pb), "v"((uint32_t)t) : "memory");
-        }
-#endif
         kstep_mma<F32, NG>(af[s], bfr, g0, s, acc);
       }
-#if DR_BALANCE
-      if constexpr (kProg) {
-        // behind the partner (ties: waves 4-7, the ones age order disfavours):
-        // priority for this tile's epilogue and the next tile's MFMA issue
-        const int ptu = __builtin_amdgcn_readfirstlane((int)pt);
-        const bool behind = ptu > t || (ptu == t && wave >= 4);
-#if DR_BALANCE == 2  // A/B: the wave AHEAD gets the priority (the hypothesis' control)
-        if (!behind) __builtin_amdgcn_s_setprio(2);
-#elif DR_BALANCE == 3  // A/B: a one-step priority difference
-        if (behind) __builtin_amdgcn_s_setprio(1);
-#else
-        if (behind) __builtin_amdgcn_s_setprio(2);
-#endif
-        else __builtin_amdgcn_s_setprio(0);
-      }
-#endif
 #else
       constexpr int HALF = KS >= 4 ? KS / 2 : KS;
 #pragma unroll
