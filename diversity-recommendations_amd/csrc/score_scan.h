@@ -88,16 +88,6 @@ enum {
 #ifndef DR_APIPE
 #define DR_APIPE 1  // A fragments read two k-steps ahead
 #endif
-#ifndef DR_TURNS
-// SIMD-pair MFMA turns: the two waves of a SIMD (w, w + 4) take strict turns
-// issuing their tiles' MFMA chains through a token in LDS (wave w on even
-// turns, w + 4 on odd ones; a wave passes the token once its chain is
-// issued, then runs its epilogue under the partner's MFMAs). Without it the
-// arbiter's age order lets waves 0-3 issue first and run ahead within a
-// stage: measured, they wait 34 % of their time at the stage barrier while
-// waves 4-7 finish alone with their epilogues exposed.
-#define DR_TURNS 0
-#endif
 #ifndef DR_FLUSH_GAP
 #define DR_FLUSH_GAP 96  // new keys a buffer takes past k + kSlack before compaction
 #endif
@@ -662,9 +652,8 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
   // user tile: the area must hold a whole wave's worth of blocks
   static_assert(!STAGED || SB >= 64, "staging area smaller than a wave");
   constexpr int WAVE_BYTES = UPW * 4 + 256 * 4 + SB * (64 + 12);
-  constexpr int TURN_BYTES = DR_TURNS ? 16 : 0;  // one token per SIMD pair
-  static_assert(RING_BYTES + kWaves * WAVE_BYTES + TURN_BYTES <= 163840, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char smem[RING_BYTES + kWaves * WAVE_BYTES + TURN_BYTES];
+  static_assert(RING_BYTES + kWaves * WAVE_BYTES <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[RING_BYTES + kWaves * WAVE_BYTES];
 
   // A buffer is compacted once it holds more than flush_at keys; a stage adds
   // at most MARGIN keys per user, so flush_at + MARGIN <= CAP. A small gap
@@ -703,17 +692,6 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
   uint64_t dg[kDgSlots] = {};
   DG_T0(t_kernel);
   const uint64_t rt_kernel = __builtin_amdgcn_s_memrealtime();  // 100 MHz: clock = cycles / time
-#endif
-#if DR_TURNS
-  // token of this wave's SIMD pair (waves w and w + 4); turns count up over
-  // the whole kernel (both waves run the same units, tiles and groups)
-  const uint32_t turn_addr = lds_ring + RING_BYTES + kWaves * WAVE_BYTES + 4u * (uint32_t)(wave & 3);
-  uint32_t turn = wave >= 4 ? 1u : 0u;
-  if (wave < 4) {
-    asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : : "v"(turn_addr), "v"(0u)
-                 : "memory");
-  }
-  // published by the first stage barrier, before any wave takes a turn
 #endif
   int64_t n_users = a.n_users, n_ublocks = a.n_ublocks;
   if (a.n_users_dev) {  // fallback rescan: only the users the guess failed
@@ -795,33 +773,6 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
       u32x4 af[KS];
       af[0] = ds_read_b128_asm(tb + a_off(0));
       if constexpr (KS > 1) af[1] = ds_read_b128_asm(tb + a_off(1));
-#if DR_TURNS
-      {  // wait for this wave's turn (the spin's lgkmcnt(0) also retires af[0..1])
-        // (a scheduling device only: no data depends on it, so after 2^20
-        // polls a wave goes on regardless — a stuck token can never hang)
-        uint32_t tv;
-        int ts, tn;
-        const uint32_t tu = __builtin_amdgcn_readfirstlane(turn);  // an SGPR operand
-        asm volatile(
-            "s_mov_b32 %2, 0x100000\n"
-            "L_turn_%=:\n\t"
-            "ds_read_b32 %0, %3\n\t"
-            "s_waitcnt lgkmcnt(0)\n\t"
-            "v_readfirstlane_b32 %1, %0\n\t"
-            "s_nop 4\n\t"
-            "s_cmp_eq_u32 %1, %4\n\t"
-            "s_cbranch_scc1 L_turn_go_%=\n\t"
-            "s_sub_u32 %2, %2, 1\n\t"
-            "s_cmp_eq_u32 %2, 0\n\t"
-            "s_cbranch_scc1 L_turn_go_%=\n\t"
-            "s_sleep 0\n\t"
-            "s_branch L_turn_%=\n"
-            "L_turn_go_%=:"
-            : "=&v"(tv), "=&s"(ts), "=&s"(tn)
-            : "v"(turn_addr), "s"(tu)
-            : "memory", "scc");
-      }
-#endif
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         if (s + 1 < KS) lds_wait1(af[s]);
@@ -829,12 +780,6 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
         if (s + 2 < KS) af[s + 2] = ds_read_b128_asm(tb + a_off(s + 2));
         kstep_mma<F32, NG>(af[s], bfr, g0, s, acc);
       }
-#if DR_TURNS
-      // the chain is issued: the partner's turn (its MFMAs queue behind ours)
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("ds_write_b32 %0, %1" : : "v"(turn_addr), "v"(turn + 1u) : "memory");
-      turn += 2u;
-#endif
 #else
       constexpr int HALF = KS >= 4 ? KS / 2 : KS;
 #pragma unroll
