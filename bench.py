@@ -283,7 +283,9 @@ def pmc_traffic(workload: str, config: str, kernel: str, group: int = 0, per_ste
     summary (tools/gpu_pmc_kernels.sh -> tools/pmc_kernels.py ->
     profiles/pmc_<workload>.json), read only when its config matches. The
     kernel's dispatches come in groups of `reps` calls (one group per phase
-    of the workload, in launch order); `per_step` = dispatches per call."""
+    of the workload, in launch order); `per_step` = dispatches per call, or 0:
+    every dispatch of the pass belongs to the workload's `reps` calls (a call
+    whose dispatch count varies, e.g. dr_score_topk's guess tiers)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     try:
         with open(path) as f:
@@ -297,9 +299,12 @@ def pmc_traffic(workload: str, config: str, kernel: str, group: int = 0, per_ste
         for name, k in rec["kernels"].items():
             if not name.startswith(prefix):
                 continue
-            part = k["hbm_bytes"][group * reps * per_step:(group + 1) * reps * per_step]
-            if len(part) != reps * per_step:
-                return None
+            if per_step == 0:
+                part = k["hbm_bytes"]
+            else:
+                part = k["hbm_bytes"][group * reps * per_step:(group + 1) * reps * per_step]
+                if len(part) != reps * per_step:
+                    return None
             total, found = total + sum(part) / reps, True
     return total if found else None
 
@@ -521,7 +526,7 @@ def main():
     cfg_key = f"U{U_n}_I{I_n}_d{d}_k{k}_G{world}"
     flops = 2.0 * (u_hi - u_lo) * (hi - lo) * d
     achieved = flops / r["topk_s"] / 1e12
-    traffic = pmc_traffic("catalog", cfg_key, SCAN_KERNELS) or load_traffic(cfg_key)
+    traffic = pmc_traffic("catalog", cfg_key, SCAN_KERNELS, per_step=0) or load_traffic(cfg_key)
     result = {
         "metric": "scored pairs/sec + ILD-eval users/sec, 1M x 10M d=128 at 1/2/4/8 GPU",
         "value": U_n * I_n / step_s,
@@ -708,7 +713,8 @@ def secondary(args):
                "items": I_n, "dim": d, "k": k},
               {"bound": "mfma", "achieved": flops / dt / 1e12, "peak": MFMA_BF16_PEAK_TFLOPS,
                "unit": "TFLOP/s", "frac": flops / dt / 1e12 / MFMA_BF16_PEAK_TFLOPS,
-               "traffic": (pmc_traffic("score1m", f"U{U_n}_I{I_n}_d{d}_k{k}_G1", SCAN_KERNELS)
+               "traffic": (pmc_traffic("score1m", f"U{U_n}_I{I_n}_d{d}_k{k}_G1", SCAN_KERNELS,
+                                       per_step=0)
                            or load_traffic(f"U{U_n}_I{I_n}_d{d}_k{k}_G1")),
                "mfma_counters": pmc_mfma("score1m", f"U{U_n}_I{I_n}_d{d}_k{k}_G1"),
                "kernel": "dr_score_topk (sample scan + thresholds + seeded scan + finalize)"}, cpu)
@@ -1211,7 +1217,7 @@ def mmr_pipeline(args):
                         "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": flops / topk_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
                         "traffic": pmc_traffic("mmr", f"mmr_U{U_n}_I{I_n}_d{d}_C{C}_k{kout}",
-                                               SCAN_KERNELS) if world == 1 else None,
+                                               SCAN_KERNELS, per_step=0) if world == 1 else None,
                         "kernel": f"dr_score_topk k={C} (the step's dominant kernel)"},
            "mmr_roofline": dict(_hbm(per_user * n_r, mmr_s,
                                      pmc_traffic("mmr", f"mmr_U{U_n}_I{I_n}_d{d}_C{C}_k{kout}",
