@@ -774,7 +774,7 @@ def secondary(args):
                "scan_width": w, "k": k},
               {"bound": "mfma", "achieved": flops_pad / dt / 1e12, "peak": MFMA_F32_PEAK_TFLOPS,
                "unit": "TFLOP/s", "frac": flops_pad / dt / 1e12 / MFMA_F32_PEAK_TFLOPS,
-               "traffic": pmc_traffic("fp32", f"fp32_U{U_n}_I{I_n}_d{d}_k{k}", SCAN_KERNELS),
+               "traffic": pmc_traffic("fp32", f"fp32_U{U_n}_I{I_n}_d{d}_k{k}", SCAN_KERNELS, per_step=0),
                "flop_per_launch": flops_pad,
                "kernel": "dr_score_topk, fp32 scan (v_mfma_f32_32x32x2_f32) + finalize; flops "
                          "counted at the padded width"},
