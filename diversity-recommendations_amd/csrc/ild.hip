@@ -143,6 +143,37 @@ __global__ __launch_bounds__(256) void ild_labels_kernel(const R* __restrict__ r
   if (lane == 0) out[u] = (float)cnt / (float)(k * (k - 1));
 }
 
+// Lists longer than the LDS staging area (the reference's user_ild takes any
+// length, intra_list_diversity_score.py:36-42): the same exact count with the
+// labels read through the cache; one wave per user.
+template <typename R>
+__global__ __launch_bounds__(256) void ild_labels_long_kernel(const R* __restrict__ recs,
+                                                              int64_t n_users, int k,
+                                                              const int64_t* __restrict__ labels,
+                                                              int64_t n_items,
+                                                              float* __restrict__ out,
+                                                              int32_t* __restrict__ err) {
+  const int lane = dr::lane_id();
+  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (u >= n_users) return;  // wave-uniform
+  const R* r = recs + u * k;
+  if (!wave_list_ok(r, k, n_items)) {  // wave-uniform
+    if (lane == 0) {
+      out[u] = __builtin_nanf("");
+      if (err) atomicAdd(err, 1);
+    }
+    return;
+  }
+  long long cnt = 0;
+  for (int p = lane; p < k; p += 64) {
+    const int64_t lp = labels[rec_at(r, p)];
+    for (int q = p + 1; q < k; ++q) cnt += (labels[rec_at(r, q)] == lp);
+  }
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) cnt += __shfl_xor(cnt, m);
+  if (lane == 0) out[u] = (float)cnt / (float)((long long)k * (k - 1));  // as the short kernel
+}
+
 // --------------------------------------------------------------- embeddings
 // One wave per user. Tile t holds rows [32t, 32t+32) of the user's list as
 // MFMA fragments: lane l -> row (l & 31), k-slice 8*(l >> 5) + 16*s. The same
@@ -258,6 +289,103 @@ __global__ __launch_bounds__(256) void ild_embedding_kernel(const R* __restrict_
   if (lane == 0) out[u] = sum / (float)(k * (k - 1));
 }
 
+// Long lists (k > 128, any width; the reference's user_ild takes any
+// length): one wave per workgroup streams the list's row tiles from the
+// cache; the per-row terms of all k rows sit in LDS (4 B each), every
+// upper-triangle Gram tile is one MFMA pass over two gathered tiles, and the
+// pair distances are summed in double (a k = 4096 list has 8.4M pairs).
+constexpr int kEmbLongMaxK = 16384;
+
+template <typename R, int D, int KIND>
+__global__ __launch_bounds__(64) void ild_embedding_long(const R* __restrict__ recs,
+                                                         int64_t n_users, int k,
+                                                         const __bf16* __restrict__ E,
+                                                         int64_t n_items,
+                                                         float* __restrict__ out,
+                                                         int32_t* __restrict__ err) {
+  constexpr int KS = D / 16;
+  __shared__ float s_w[kEmbLongMaxK];  // per row: 1/|e| (cosine) or |e|^2 (euclidean)
+  const int lane = dr::lane_id();
+  const int h = lane >> 5, col = lane & 31;
+  const int64_t u = blockIdx.x;
+  const R* r = recs + u * k;
+  if (!wave_list_ok(r, k, n_items)) {  // wave-uniform
+    if (lane == 0) {
+      out[u] = __builtin_nanf("");
+      if (err) atomicAdd(err, 1);
+    }
+    return;
+  }
+  const int nt = (k + 31) / 32;
+  auto load = [&](int t, bf16x8 (&f)[KS]) {
+    const int p = 32 * t + col;
+    const int64_t row = rec_at(r, p < k ? p : 0);
+    const uint4* src = reinterpret_cast<const uint4*>(E + row * D + 8 * h);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) f[s] = __builtin_bit_cast(bf16x8, src[2 * s]);
+  };
+  if constexpr (KIND != DR_ILD_DOT) {
+    for (int t = 0; t < nt; ++t) {
+      bf16x8 x[KS];
+      load(t, x);
+      const f32x16 g = gram_tile<D>(x, x);
+      const int ri = (col & 3) + 4 * (col >> 3);
+      float v = g[0];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) v = (ri == q) ? g[q] : v;
+      if (KIND == DR_ILD_COSINE) v = 1.f / sqrtf(v);
+      if (((col >> 2) & 1) == h && 32 * t + col < k) s_w[32 * t + col] = v;
+    }
+    __syncthreads();
+  }
+  double sum = 0.0;
+  for (int ti = 0; ti < nt; ++ti) {
+    bf16x8 x[KS];
+    load(ti, x);
+    float wi[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = 32 * ti + (q & 3) + 8 * (q >> 2) + 4 * h;
+      wi[q] = (KIND != DR_ILD_DOT && i < k) ? s_w[i] : 0.f;
+    }
+    for (int tj = ti; tj < nt; ++tj) {
+      bf16x8 y[KS];
+      load(tj, y);
+      const f32x16 g = gram_tile<D>(x, y);  // g[q] = <e_i, e_j>, i = row, j = col
+      const int j = 32 * tj + col;
+      const bool jv = j < k;
+      const float wj = (KIND != DR_ILD_DOT && jv) ? s_w[j] : 0.f;
+      float part = 0.f;  // <= 16 terms in fp32, the tile sums in double
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = 32 * ti + (q & 3) + 8 * (q >> 2) + 4 * h;
+        const bool ok = jv && (ti < tj || i < j);
+        float dist;
+        if constexpr (KIND == DR_ILD_COSINE) dist = fmaf(-g[q], wi[q] * wj, 1.f);
+        else if constexpr (KIND == DR_ILD_DOT) dist = g[q];
+        else dist = sqrtf(fmaxf(wi[q] + wj - 2.f * g[q], 0.f));
+        part += ok ? dist : 0.f;
+      }
+      sum += (double)part;
+    }
+  }
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) sum += __shfl_xor(sum, m);
+  if (lane == 0) out[u] = (float)(sum / ((double)k * (double)(k - 1)));
+}
+
+template <typename R, int D>
+void launch_long(const R* recs, int64_t n_users, int k, const __bf16* E, int64_t ni, int kind,
+                 float* out, int32_t* err, hipStream_t s) {
+  const dim3 grid((unsigned)n_users);
+  if (kind == DR_ILD_COSINE)
+    hipLaunchKernelGGL((ild_embedding_long<R, D, DR_ILD_COSINE>), grid, 64, 0, s, recs, n_users, k, E, ni, out, err);
+  else if (kind == DR_ILD_DOT)
+    hipLaunchKernelGGL((ild_embedding_long<R, D, DR_ILD_DOT>), grid, 64, 0, s, recs, n_users, k, E, ni, out, err);
+  else
+    hipLaunchKernelGGL((ild_embedding_long<R, D, DR_ILD_EUCLIDEAN>), grid, 64, 0, s, recs, n_users, k, E, ni, out, err);
+}
+
 // Register-resident variant for nt = NT row tiles: every row of the list is
 // gathered into MFMA fragments up front (all loads in flight together), then
 // the norms and the upper-triangle Gram tiles are formed from registers. The
@@ -370,6 +498,17 @@ template <typename R>
 int launch_embedding(const R* recs, int64_t n_users, int k, const __bf16* E, int64_t ni, int d,
                      int kind, float* out, int32_t* err, hipStream_t s) {
   const int grid = (int)dr::ceil_div(n_users, 4);
+  if (k > kEmbMaxK) {  // long lists: the streaming kernel, any width
+    switch (d) {
+      case 32: launch_long<R, 32>(recs, n_users, k, E, ni, kind, out, err, s); return DR_OK;
+      case 64: launch_long<R, 64>(recs, n_users, k, E, ni, kind, out, err, s); return DR_OK;
+      case 128: launch_long<R, 128>(recs, n_users, k, E, ni, kind, out, err, s); return DR_OK;
+      case 256: launch_long<R, 256>(recs, n_users, k, E, ni, kind, out, err, s); return DR_OK;
+      default:
+        dr::set_error("dr_ild_embedding: d must be one of 32, 64, 128, 256");
+        return DR_EUNSUPPORTED;
+    }
+  }
   // the whole list fits in registers for d <= 128 (k <= 128 = 4 tiles)
   if (d == 32 || d == 64 || d == 128) {
     if (d == 32) launch_regs<R, 32>(recs, n_users, k, E, ni, kind, out, err, s, grid);
@@ -462,18 +601,23 @@ extern "C" int dr_ild_dense_pair_sum(const void* recs, int rec_dtype, int64_t n_
 extern "C" int dr_ild_labels(const void* recs, int rec_dtype, int64_t n_users, int k,
                              const int64_t* labels, int64_t n_items, float* out, int32_t* err,
                              dr_stream_t stream) {
-  DR_CHECK_ARG(k >= 1 && k <= kLabelMaxK, "k must be in [1, 1024]");
+  DR_CHECK_ARG(k >= 1, "k must be >= 1");
   DR_CHECK_ARG(rec_dtype == DR_I32 || rec_dtype == DR_I64, "rec_dtype must be DR_I32/DR_I64");
   if (n_users == 0) return DR_OK;
   DR_CHECK_ARG(recs && labels && out, "null pointer");
   hipStream_t s = (hipStream_t)stream;
   const int grid = (int)dr::ceil_div(n_users, 4);
-  if (rec_dtype == DR_I32)
-    hipLaunchKernelGGL((ild_labels_kernel<int32_t>), grid, 256, 0, s, (const int32_t*)recs,
-                       n_users, k, labels, n_items, out, err);
-  else
-    hipLaunchKernelGGL((ild_labels_kernel<int64_t>), grid, 256, 0, s, (const int64_t*)recs,
-                       n_users, k, labels, n_items, out, err);
+#define DR_LAB(KERN, RT)                                                                   \
+  hipLaunchKernelGGL((KERN<RT>), grid, 256, 0, s, (const RT*)recs, n_users, k, labels, \
+                     n_items, out, err)
+  if (k <= kLabelMaxK) {  // the list's labels staged in LDS
+    if (rec_dtype == DR_I32) DR_LAB(ild_labels_kernel, int32_t);
+    else DR_LAB(ild_labels_kernel, int64_t);
+  } else {
+    if (rec_dtype == DR_I32) DR_LAB(ild_labels_long_kernel, int32_t);
+    else DR_LAB(ild_labels_long_kernel, int64_t);
+  }
+#undef DR_LAB
   DR_CHECK_LAUNCH();
   return DR_OK;
 }
@@ -481,7 +625,7 @@ extern "C" int dr_ild_labels(const void* recs, int rec_dtype, int64_t n_users, i
 extern "C" int dr_ild_embedding(const void* recs, int rec_dtype, int64_t n_users, int k,
                                 const void* item_table, int64_t n_items, int d, int kind,
                                 float* out, int32_t* err, dr_stream_t stream) {
-  DR_CHECK_ARG(k >= 1 && k <= kEmbMaxK, "k must be in [1, 128]");
+  DR_CHECK_ARG(k >= 1 && k <= kEmbLongMaxK, "k must be in [1, 16384]");
   DR_CHECK_ARG(rec_dtype == DR_I32 || rec_dtype == DR_I64, "rec_dtype must be DR_I32/DR_I64");
   DR_CHECK_ARG(kind == DR_ILD_COSINE || kind == DR_ILD_DOT || kind == DR_ILD_EUCLIDEAN,
                "unknown distance kind");

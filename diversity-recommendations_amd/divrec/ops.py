@@ -370,7 +370,6 @@ def ild_labels(recs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     recs, rc_dt = _recs(recs)
     labels = labels.to(torch.int64).contiguous()
     n, k = recs.shape
-    _need(k <= 1024, "k must be <= 1024")
     out = torch.empty(n, dtype=torch.float32, device=dev)
     if n == 0:
         return out
@@ -432,7 +431,7 @@ def ild_embedding(recs: torch.Tensor, item_table: torch.Tensor, kind: str = "cos
     item_table = pad_columns_cached(item_table,
                                     _width_of(ILD_WIDTHS, item_table.size(1), "embedding ILD"))
     n, k = recs.shape
-    _need(k <= 128, "embedding ILD supports k <= 128")
+    _need(k <= 16384, "embedding ILD supports k <= 16384")
     out = torch.empty(n, dtype=torch.float32, device=dev)
     if n == 0:
         return out

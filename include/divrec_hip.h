@@ -205,14 +205,17 @@ int dr_ild_dense_pair_sum(const void* recs, int rec_dtype, int64_t n_users, int 
 
 /* Label equality D[i,j] = (label[i] == label[j]), the matrix of
  * IntraListBinaryUnfairnessScore.get_distance_matrix (:60-63), computed on the
- * fly from labels int64 [n_items] (exact integer count). */
+ * fly from labels int64 [n_items] (exact integer count). Any k: lists of up to
+ * 1024 stage their labels in LDS, longer ones read them through the cache. */
 int dr_ild_labels(const void* recs, int rec_dtype, int64_t n_users, int k,
                   const int64_t* labels, int64_t n_items, float* out, int32_t* err,
                   dr_stream_t stream);
 
 /* Distance computed on the fly from an item embedding table (bf16 [n_items, d],
- * d in {32, 64, 128, 256}, k <= 128) by a bf16 MFMA Gram tile per user
- * (kind: enum dr_ild_kind). fp32 accumulation. */
+ * d in {32, 64, 128, 256}, 1 <= k <= 16384) by bf16 MFMA Gram tiles per user
+ * (kind: enum dr_ild_kind). k <= 128: the list in registers, fp32 accumulation;
+ * longer lists (the reference's user_ild takes any length): the row tiles
+ * streamed through the cache, tile sums accumulated in double. */
 int dr_ild_embedding(const void* recs, int rec_dtype, int64_t n_users, int k,
                      const void* item_table, int64_t n_items, int d, int kind, float* out,
                      int32_t* err, dr_stream_t stream);
