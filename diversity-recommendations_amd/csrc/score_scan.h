@@ -290,31 +290,13 @@ __device__ __forceinline__ int lane_prefix(uint64_t bal) {  // set bits of bal b
                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 }
 
-#ifndef DR_MAX3_ASM
-#define DR_MAX3_ASM 0  // A/B: the epilogue's 16-way max as 8 v_max3_f32 without canonicalising copies
-#endif
-// Max of a lane's 16 scores of one user tile (the hot test). fmaxf makes
-// hipcc quiet possible signalling NaNs first (a v_max_f32 x, x per leading
-// operand); MFMA results are never signalling NaNs, and IEEE-mode v_max3_f32
-// returns the non-NaN operand for a quiet one, so DR_MAX3_ASM skips the copies.
+// Max of a lane's 16 scores of one user tile (the hot test); hipcc forms
+// v_max3_f32 from the chain.
 __device__ __forceinline__ float max16(const f32x16& a) {
-#if DR_MAX3_ASM
-  float m0, m1, m2, m3, m4, m5, m6, m;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m0) : "v"(a[0]), "v"(a[1]), "v"(a[2]));
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m1) : "v"(a[3]), "v"(a[4]), "v"(a[5]));
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m2) : "v"(a[6]), "v"(a[7]), "v"(a[8]));
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m3) : "v"(a[9]), "v"(a[10]), "v"(a[11]));
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m4) : "v"(a[12]), "v"(a[13]), "v"(a[14]));
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m5) : "v"(m0), "v"(m1), "v"(a[15]));
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m6) : "v"(m2), "v"(m3), "v"(m4));
-  asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(m5), "v"(m6));
-  return m;
-#else
   float m = a[0];
 #pragma unroll
   for (int r = 1; r < 16; ++r) m = fmaxf(m, a[r]);
   return m;
-#endif
 }
 
 struct CompactResult {
