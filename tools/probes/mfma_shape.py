@@ -1,6 +1,7 @@
 """Run tools/probes/mfma_shape.hip: TFLOP/s of bare 32x32x16 and 16x16x32 bf16
 MFMA loops on random operands, one 512-thread workgroup per CU, each shape
-timed for ~2 s of sustained load (three alternating rounds). Prints one JSON line.
+timed on one ~2.7-ms launch per round, three alternating rounds. Prints one
+JSON line.
 
     hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/probes/mfma_shape.hip -o tools/probes/libmfma_shape.so
     python tools/probes/mfma_shape.py
