@@ -116,6 +116,9 @@ enum {
 #endif
 constexpr int kWaves = DR_WAVES;
 constexpr int kThreads = kWaves * 64;
+// Longest catalog a staged (W <= 64) scan takes: its staged blocks name their
+// tile in 23 bits (dr_score_topk refuses longer ones).
+constexpr int64_t kMaxStagedRows = (int64_t)32 << 23;
 constexpr int kTileItems = 32;
 #ifndef DR_SLACK
 #define DR_SLACK 32
@@ -290,14 +293,36 @@ __device__ __forceinline__ int lane_prefix(uint64_t bal) {  // set bits of bal b
                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 }
 
-// Max of a lane's 16 scores of one user tile (the hot test); hipcc forms
-// v_max3_f32 from the chain.
+// Max of a lane's 16 scores of one user tile, as a VALUE (stored in keys):
+// IEEE maxNum, NaN scores ignored; hipcc forms v_max3_f32 from the chain, with
+// canonicalising copies of the MFMA results in front (10 VALU per tile).
 __device__ __forceinline__ float max16(const f32x16& a) {
   float m = a[0];
 #pragma unroll
   for (int r = 1; r < 16; ++r) m = fmaxf(m, a[r]);
   return m;
 }
+
+#ifndef DR_HOT_MAXIMUM
+#define DR_HOT_MAXIMUM 1  // hot test on v_maximum3_f32 (0: the maxNum chain above)
+#endif
+// The hot test's max: IEEE-754-2019 maximum (gfx950 v_maximum3_f32: NaN
+// propagates, no operand canonicalisation), 8 VALU per tile instead of 10.
+// Only ever compared through hot(): a NaN max counts as a hit, so the exact
+// per-score tests behind it see the tile (NaN scores are never admitted there,
+// as with maxNum, where they were skipped by the max).
+__device__ __forceinline__ float hot_max16(const f32x16& a) {
+#if DR_HOT_MAXIMUM
+  float m = __builtin_elementwise_maximum(a[0], a[1]);
+#pragma unroll
+  for (int r = 2; r < 16; ++r) m = __builtin_elementwise_maximum(m, a[r]);
+  return m;
+#else
+  return max16(a);
+#endif
+}
+// "some score of the tile may beat thr": a superset of `max > thr` (NaN = hit)
+__device__ __forceinline__ bool hot(float m, float thr) { return !(m <= thr); }
 
 struct CompactResult {
   int kept;
@@ -654,13 +679,14 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
   constexpr int kLpt = G::LPT;
   constexpr int RING_BYTES = kRing * kStageBytes;
   // per wave: per-user key counts, radix histogram, staged survivor blocks
-  // (16 scores + item base + slot + threshold each)
+  // (16 scores + one 8-B record: tile | slot | h, threshold)
   constexpr bool STAGED = DR_ENQ_STAGED == 1 || (DR_ENQ_STAGED == 2 && D <= 64);
   constexpr int SB = STAGED ? DR_STAGE_BLOCKS : 0;
   // stage_hits resolves a full stage area, then stages up to 64 lanes of one
   // user tile: the area must hold a whole wave's worth of blocks
   static_assert(!STAGED || SB >= 64, "staging area smaller than a wave");
-  constexpr int WAVE_BYTES = UPW * 4 + 256 * 4 + SB * (64 + 12);
+  static_assert(!STAGED || NU_T * 32 <= 256, "staged slot field is 8 bits");
+  constexpr int WAVE_BYTES = UPW * 4 + 256 * 4 + SB * (64 + 8);
   static_assert(RING_BYTES + kWaves * WAVE_BYTES <= 163840, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[RING_BYTES + kWaves * WAVE_BYTES];
 
@@ -686,9 +712,10 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
   uint32_t* ucnt = reinterpret_cast<uint32_t*>(wbase);
   uint32_t* hist = reinterpret_cast<uint32_t*>(wbase + UPW * 4);
   float* blk_val = reinterpret_cast<float*>(wbase + UPW * 4 + 1024);  // [SB][16], 16-B aligned
-  uint32_t* blk_gbase = reinterpret_cast<uint32_t*>(blk_val + SB * 16);
-  uint32_t* blk_slot = blk_gbase + SB;  // slot | h << 16 | valid rows << 17
-  float* blk_thr = reinterpret_cast<float*>(blk_slot + SB);
+  // [SB] {tile of the unit | slot << 23 | h << 31, threshold bits}: one
+  // ds_write_b64 per staged lane; 23 tile bits cover kMaxStagedRows (the host
+  // refuses longer catalogs at the staged widths)
+  uint2* blk_meta = reinterpret_cast<uint2*>(blk_val + SB * 16);
   const uint32_t lds_ring = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
   // This lane's A-fragment byte offset for k-step s in a tile is
   // col*2D + ((2s + h) ^ swz(col)) * 16 = a_row + ((2s) ^ a_sw) * 16: two VALU
@@ -850,15 +877,17 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
 
     // -------------------------------------------------------------- epilogues
     // Hot test (branch-free): per user tile, a 16-way max against the threshold.
-    auto any_hits = [&](f32x16 (&acc)[NG], auto GI) -> uint32_t {
+    // The per-tile ballots are the v_cmp results themselves (SGPR pairs); their
+    // OR is the one uniform branch of the common no-hit case.
+    auto any_hits = [&](f32x16 (&acc)[NG], uint64_t (&hb)[NG], auto GI) -> uint64_t {
       constexpr int g0 = decltype(GI)::value * NG;
-      uint32_t bits = 0;
+      uint64_t any = 0ull;
 #pragma unroll
       for (int ut = 0; ut < NG; ++ut) {
-        float m = max16(acc[ut]);
-        bits |= (__ballot(m > thr[g0 + ut]) != 0ull ? 1u : 0u) << ut;
+        hb[ut] = __ballot(hot(hot_max16(acc[ut]), thr[g0 + ut]));
+        any |= hb[ut];
       }
-      return bits;
+      return any;
     };
 
     // Append survivors straight to their users' candidate buffers in HBM: one
@@ -866,7 +895,7 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
     // call and no queue in the hot loop, so nothing forces the accumulators
     // and B fragments out of registers. A stage adds at most MARGIN keys per
     // user, so a buffer compacted at the stage end never overflows.
-    auto enqueue = [&](int t, f32x16 (&acc)[NG], uint32_t hit_bits, auto GI) {
+    auto enqueue = [&](int t, f32x16 (&acc)[NG], const uint64_t (&hb)[NG], auto GI) {
       constexpr int g0 = decltype(GI)::value * NG;
       DG_T0(t_e);
       const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
@@ -883,7 +912,7 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
       }
 #pragma unroll
       for (int ut = 0; ut < NG; ++ut) {
-        if (!(hit_bits & (1u << ut))) continue;
+        if (hb[ut] == 0ull) continue;
         uint32_t mask = 0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) mask |= (acc[ut][r] > thr[g0 + ut] ? 1u : 0u) << r;
@@ -975,12 +1004,15 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
         const int i = b0 + lane;
         const bool live = i < nblk;
         const int ii = live ? i : 0;
-        const uint32_t gb = blk_gbase[ii];
-        const uint32_t info = blk_slot[ii];  // slot | h << 16 | valid rows << 17
-        const float th = blk_thr[ii];
-        const uint32_t slot = info & 0xffffu;
-        const int hh = (int)((info >> 16) & 1u);
-        const int vld = live ? (int)(info >> 17) : 0;
+        const uint2 meta = blk_meta[ii];
+        const uint32_t tl = meta.x & 0x7fffffu;  // tile of the unit
+        const uint32_t slot = (meta.x >> 23) & 0xffu;
+        const int hh = (int)(meta.x >> 31);
+        const float th = __uint_as_float(meta.y);
+        const int64_t row0 = i_beg + (int64_t)tl * kTileItems;
+        const uint32_t gb = (uint32_t)(a.item_base + row0);
+        const int64_t left = i_end - row0;  // rows past the slice end are not scores
+        const int vld = live ? (left < kTileItems ? (int)left : kTileItems) : 0;
         uint64_t* ubuf = cbase + (size_t)slot * CAP;
         const float4* src = reinterpret_cast<const float4*>(blk_val + ii * 16);
         if constexpr (decltype(BATCHED)::value != 0) {
@@ -1053,7 +1085,7 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
       DG_ADD(kDgDrain, t_d);
       DG_CNT(kDgNDrain);
     };
-    auto stage_hits = [&](int t, f32x16 (&acc)[NG], uint32_t hit_bits, auto GI) {
+    auto stage_hits = [&](int t, f32x16 (&acc)[NG], const uint64_t (&hb)[NG], auto GI) {
       constexpr int g0 = decltype(GI)::value * NG;
       DG_T0(t_e);
       const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
@@ -1061,9 +1093,9 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
       const uint32_t gbase = (uint32_t)(a.item_base + tile0);
 #pragma unroll
       for (int ut = 0; ut < NG; ++ut) {
-        if (!(hit_bits & (1u << ut))) continue;
-        float m = max16(acc[ut]);
-        const bool hit = m > thr[g0 + ut];
+        if (hb[ut] == 0ull) continue;
+        float m = hot_max16(acc[ut]);
+        const bool hit = hot(m, thr[g0 + ut]);
         const uint64_t bal = __ballot(hit);
         if (bal == 0ull) continue;
         const int n = __popcll(bal);
@@ -1075,10 +1107,9 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
           for (int q = 0; q < 4; ++q)
             dst[q] = make_float4(acc[ut][4 * q], acc[ut][4 * q + 1], acc[ut][4 * q + 2],
                                  acc[ut][4 * q + 3]);
-          blk_gbase[i] = gbase;
-          blk_slot[i] =
-              (uint32_t)((g0 + ut) * 32 + col) | ((uint32_t)h << 16) | ((uint32_t)valid << 17);
-          blk_thr[i] = thr[g0 + ut];
+          blk_meta[i] = make_uint2((uint32_t)t | ((uint32_t)((g0 + ut) * 32 + col) << 23) |
+                                       ((uint32_t)h << 31),
+                                   __float_as_uint(thr[g0 + ut]));
         }
         nblk += n;
       }
@@ -1120,18 +1151,18 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
         return;
       }
       DG_T0(t_h);
-      uint32_t hit_bits = any_hits(acc, GI);
+      uint64_t hb[NG];
+      const uint64_t any = any_hits(acc, hb, GI);
       DG_ADD(kDgHits, t_h);
-      hit_bits = __builtin_amdgcn_readfirstlane(hit_bits);  // ballots: uniform
       if constexpr (STAGED) {
-        if (hit_bits != 0u) stage_hits(t, acc, hit_bits, GI);
+        if (any != 0ull) stage_hits(t, acc, hb, GI);
         // end of a stage: resolve the staged blocks, compact full buffers
         if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) {
           if (nblk > 0) resolve(IC<DR_RESOLVE_BATCHED>{});
           check_compact(flush_at, a.slack);
         }
       } else {
-        if (hit_bits != 0u) enqueue(t, acc, hit_bits, GI);
+        if (any != 0ull) enqueue(t, acc, hb, GI);
         // end of a stage: compact the buffers that passed flush_at
         if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles))
           check_compact(flush_at, a.slack);
@@ -1154,12 +1185,12 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
       };
       auto epi = [&](int t, f32x16 (&acc)[NG], auto GI) {
         DG_T0(t_h);
-        uint32_t hit_bits = any_hits(acc, GI);
+        uint64_t hb[NG];
+        const uint64_t any = any_hits(acc, hb, GI);
         DG_ADD(kDgHits, t_h);
-        hit_bits = __builtin_amdgcn_readfirstlane(hit_bits);
-        if (hit_bits != 0u) {
-          if constexpr (STAGED) stage_hits(t, acc, hit_bits, GI);
-          else enqueue(t, acc, hit_bits, GI);
+        if (any != 0ull) {
+          if constexpr (STAGED) stage_hits(t, acc, hb, GI);
+          else enqueue(t, acc, hb, GI);
         }
       };
       for (int t = 0; t < ntiles; ++t) {
