@@ -16,6 +16,10 @@ namespace dr {
 // Thread-local last-error string behind dr_last_error() (include/divrec_hip.h).
 void set_error(const std::string& msg);
 
+// Planner knobs (dr_set_plan_knob, include/divrec_hip.h): true and *v set when
+// knob `id` holds a value (not NaN).
+bool plan_knob(int id, double* v);
+
 #define DR_CHECK_ARG(cond, msg)                                   \
   do {                                                            \
     if (!(cond)) {                                                \

@@ -304,7 +304,10 @@ __global__ __launch_bounds__(64) void ild_embedding_long(const R* __restrict__ r
                                                          float* __restrict__ out,
                                                          int32_t* __restrict__ err) {
   constexpr int KS = D / 16;
-  __shared__ float s_w[kEmbLongMaxK];  // per row: 1/|e| (cosine) or |e|^2 (euclidean)
+  // per row: 1/|e| (cosine) or |e|^2 (euclidean); sized by the launch to k
+  // floats (none for dot products), so a list of 129 rows keeps the CU's LDS
+  // for other workgroups
+  extern __shared__ float s_w[];
   const int lane = dr::lane_id();
   const int h = lane >> 5, col = lane & 31;
   const int64_t u = blockIdx.x;
@@ -378,12 +381,13 @@ template <typename R, int D>
 void launch_long(const R* recs, int64_t n_users, int k, const __bf16* E, int64_t ni, int kind,
                  float* out, int32_t* err, hipStream_t s) {
   const dim3 grid((unsigned)n_users);
+  const size_t lds = (size_t)k * sizeof(float);  // k <= kEmbLongMaxK: at most 64 KB
   if (kind == DR_ILD_COSINE)
-    hipLaunchKernelGGL((ild_embedding_long<R, D, DR_ILD_COSINE>), grid, 64, 0, s, recs, n_users, k, E, ni, out, err);
+    hipLaunchKernelGGL((ild_embedding_long<R, D, DR_ILD_COSINE>), grid, 64, lds, s, recs, n_users, k, E, ni, out, err);
   else if (kind == DR_ILD_DOT)
     hipLaunchKernelGGL((ild_embedding_long<R, D, DR_ILD_DOT>), grid, 64, 0, s, recs, n_users, k, E, ni, out, err);
   else
-    hipLaunchKernelGGL((ild_embedding_long<R, D, DR_ILD_EUCLIDEAN>), grid, 64, 0, s, recs, n_users, k, E, ni, out, err);
+    hipLaunchKernelGGL((ild_embedding_long<R, D, DR_ILD_EUCLIDEAN>), grid, 64, lds, s, recs, n_users, k, E, ni, out, err);
 }
 
 // Register-resident variant for nt = NT row tiles: every row of the list is

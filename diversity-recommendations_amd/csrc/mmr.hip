@@ -795,7 +795,7 @@ namespace {
 #endif
 
 // CUs of the current device (cached per device ordinal: a process may drive
-// GPUs of different sizes); DIVREC_SCAN_SLOTS, the planner's test knob, caps
+// GPUs of different sizes); DR_KNOB_SCAN_SLOTS, the planner's test knob, caps
 // the grid so that tests reach many users per workgroup with few users.
 int grid_cus() {
   static std::atomic<int> cache[64];
@@ -808,10 +808,8 @@ int grid_cus() {
       n = 256;
     if (dev >= 0 && dev < 64) cache[dev].store(n, std::memory_order_relaxed);
   }
-  if (const char* e = getenv("DIVREC_SCAN_SLOTS")) {
-    const int v = atoi(e);
-    if (v > 0 && v < n) n = v;
-  }
+  double v;
+  if (dr::plan_knob(DR_KNOB_SCAN_SLOTS, &v) && v > 0 && (int)v < n) n = (int)v;
   return n;
 }
 

@@ -348,14 +348,17 @@ int p_for(int total) {
 
 // ------------------------------------------------------------------ planning
 // Plans take w, the row width in bf16 units (d for bf16 tables, 2d for fp32).
-// Workgroup slots = CUs (one 512-thread workgroup per CU). DIVREC_SCAN_SLOTS
+// Workgroup slots = CUs (one 512-thread workgroup per CU). DR_KNOB_SCAN_SLOTS
 // overrides the count so that tests can reach the split-tail plans with
 // small inputs; the result is identical for any plan.
+int knob_int(int id, int fallback) {
+  double v;
+  return dr::plan_knob(id, &v) ? (int)v : fallback;
+}
+
 int device_cus() {
-  if (const char* e = getenv("DIVREC_SCAN_SLOTS")) {
-    const int v = atoi(e);
-    if (v > 0) return v;
-  }
+  const int slots = knob_int(DR_KNOB_SCAN_SLOTS, 0);
+  if (slots > 0) return slots;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -434,12 +437,12 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   int best_c = 1;
   double best = (double)H / slots + (double)dr::ceil_div(T, slots);
   int max_c = max_c_override > 0 ? max_c_override : kMaxTailChunks;
-  if (const char* e = getenv("DIVREC_SCAN_SPLIT")) max_c = atoi(e) > 0 ? atoi(e) : 1;  // A/B knob
+  if (const int c = knob_int(DR_KNOB_SCAN_SPLIT, 0); c != 0) max_c = c > 0 ? c : 1;  // A/B knob
   // a head user's finalize already sorts 2048 keys when its flush bound
   // passes 1024 (k >= ~800): the tail may then gather as many
   const int head_flush = std::min(k + kSlack + kFlushGap, p.cap - (int)stage_items);
   int max_keys = head_flush > kMaxTailKeys ? 2048 : kMaxTailKeys;
-  if (const char* e = getenv("DIVREC_TAIL_KEYS")) max_keys = atoi(e) > 0 ? atoi(e) : max_keys;  // A/B knob
+  if (const int m = knob_int(DR_KNOB_TAIL_KEYS, 0); m > 0) max_keys = m;  // A/B knob
   for (int c = 2; c <= max_c && T > 0; ++c) {
     if (n_items / c < min_chunk) break;
     if (c * k > max_keys) break;  // each chunk keeps at least k keys
@@ -552,10 +555,9 @@ constexpr int64_t kGuessMaxItems = 1ll << DR_GUESS_MAX_LOG2;
 Guess guess_for(int64_t n_items, int k, bool split_tail) {
   Guess g;
   if (!DR_GUESS || n_items < kGuessMinItems) return g;
-  const char* force = getenv("DIVREC_SCAN_SEED");  // A/B knob: "0" never, "1" always
-  if (force && force[0] == '0') return g;
-  if (n_items > kGuessMaxItems && k < DR_GUESS_LONG_K && !split_tail && !(force && force[0] == '1'))
-    return g;
+  const int force = knob_int(DR_KNOB_SCAN_SEED, -1);  // A/B knob: 0 never, 1 always
+  if (force == 0) return g;
+  if (n_items > kGuessMaxItems && k < DR_GUESS_LONG_K && !split_tail && force != 1) return g;
   // Long catalogs sample more sparsely: the sample scan starts from -inf and
   // is survivor-dense (~1.5x the per-row cost of the seeded scan), so about
   // 2^16 sample rows are kept (stride 32 up to 2^22 rows, 64 from 4.2M,
@@ -564,7 +566,7 @@ Guess guess_for(int64_t n_items, int k, bool split_tail) {
   // (profiles/r02_scan/ab_stride_10m.json). Long lists keep stride 32.
   g.stride = kGuessStride;
   while (k < DR_GUESS_LONG_K && g.stride < 128 && n_items / (2 * g.stride) >= 65536) g.stride *= 2;
-  if (const char* e = getenv("DIVREC_GUESS_STRIDE")) g.stride = atoi(e) > 1 ? atoi(e) : g.stride;  // A/B knob
+  if (const int st = knob_int(DR_KNOB_GUESS_STRIDE, 0); st > 1) g.stride = st;  // A/B knob
   // a whole number of 32-row tiles: the sample is stored tile-transposed
   // (sample_rows_kernel), and rows left out only lower the sample's order
   // statistics, so the guess stays a lower bound
@@ -573,12 +575,11 @@ Guess guess_for(int64_t n_items, int k, bool split_tail) {
   int ks = (int)ceil(mu + DR_GUESS_SIGMA * sqrt(mu) + 3.0);
   g.ks = ks < k ? ks : k;
   double z1 = DR_GUESS_TIGHT_Z, c1 = 1.0;
-  if (const char* e = getenv("DIVREC_GUESS_Z1")) z1 = atof(e);  // A/B knobs
-  if (const char* e = getenv("DIVREC_GUESS_C1")) c1 = atof(e);
+  dr::plan_knob(DR_KNOB_GUESS_Z1, &z1);  // A/B knobs
+  dr::plan_knob(DR_KNOB_GUESS_C1, &c1);
   int ks1 = (int)ceil(mu + z1 * sqrt(mu) + c1);
   if (ks1 < 1) ks1 = 1;
-  const char* tight = getenv("DIVREC_GUESS_TIGHT");  // A/B knob: "0" = one tier (ks1 = ks)
-  if (tight && tight[0] == '0') ks1 = g.ks;
+  if (knob_int(DR_KNOB_GUESS_TIGHT, 1) == 0) ks1 = g.ks;  // A/B knob: one tier (ks1 = ks)
   g.ks1 = ks1 < g.ks ? ks1 : g.ks;
   return g;
 }

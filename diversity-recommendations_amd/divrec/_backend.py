@@ -6,10 +6,12 @@ every call raises ``RuntimeError`` — loudly, never silently degrading.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import math
 import os
 from pathlib import Path
-from typing import Optional
+from typing import Iterator, Optional
 
 import torch
 
@@ -40,6 +42,8 @@ SIGNATURES = {
     "dr_version": (_i32, []),
     "dr_build_id": (ctypes.c_char_p, []),
     "dr_last_error": (ctypes.c_char_p, []),
+    "dr_set_plan_knob": (_i32, [_i32, _f64]),
+    "dr_get_plan_knob": (_f64, [_i32]),
     "dr_gather_dot": (_i32, [_p, _i64, _p, _i64, _i32, _i64, _p, _p, _i64, _p, _p, _p]),
     "dr_gather_dot_backward": (_i32, [_p, _i64, _p, _i64, _i64, _p, _p, _i64, _p, _p, _p, _p,
                                       _p]),
@@ -187,3 +191,32 @@ def dtype_code(dt: torch.dtype) -> int:
         return _DTYPE_CODE[dt]
     except KeyError:
         raise RuntimeError(f"unsupported dtype {dt}") from None
+
+
+# Planner knobs (include/divrec_hip.h enum dr_plan_knob): tests and A/B runs
+# only; every plan gives identical results.
+PLAN_KNOBS = {
+    "scan_slots": 0, "scan_split": 1, "tail_keys": 2, "scan_seed": 3,
+    "guess_stride": 4, "guess_z1": 5, "guess_c1": 6, "guess_tight": 7,
+}
+
+
+@contextlib.contextmanager
+def plan_knobs(**knobs: float) -> Iterator[None]:
+    """Set dr_score_topk planner knobs (names of PLAN_KNOBS) for the duration
+    of the block, restoring the previous values after it. The knobs are
+    process-wide: the block should not overlap other threads' scoring calls."""
+    L = lib()
+    ids = {}
+    for name, value in knobs.items():
+        if name not in PLAN_KNOBS:
+            raise ValueError(f"unknown planner knob {name!r}; known: {sorted(PLAN_KNOBS)}")
+        ids[PLAN_KNOBS[name]] = float(value)
+    old = {i: L.dr_get_plan_knob(i) for i in ids}
+    try:
+        for i, v in ids.items():
+            check(L.dr_set_plan_knob(i, v), "dr_set_plan_knob")
+        yield
+    finally:
+        for i, v in old.items():
+            L.dr_set_plan_knob(i, v if not math.isnan(v) else math.nan)

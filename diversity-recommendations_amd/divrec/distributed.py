@@ -258,9 +258,13 @@ def global_thresholds(user_table: torch.Tensor, item_shard: torch.Tensor, lo: in
     sample = comm.all_gather_rows(rows.contiguous(), sizes)
     n = user_table.size(0) if user_ids is None else user_ids.numel()
     u_lo, u_hi = shard_range(n, world, rank)
-    ks1, ks = guess_ranks(k, sample.size(0) / n_items) if sample.size(0) else (0, 0)
+    # dr_sample_thresholds ranks the whole 32-row tiles of the sample only, and
+    # guess_for takes mu from that rounded count: so does the HIP path here
+    # (ADVICE r4), the two tiers then sit at the single-GPU guess's ranks
+    n_s = sample.size(0) // 32 * 32 if sample_thr is not None else sample.size(0)
+    ks1, ks = guess_ranks(k, n_s / n_items) if n_s else (0, 0)
     thr = torch.full((u_hi - u_lo, 2), -math.inf, dtype=torch.float32, device=user_table.device)
-    if ks and u_hi > u_lo and sample.size(0) >= ks:
+    if ks and u_hi > u_lo and n_s >= ks:
         ids = (user_ids[u_lo:u_hi] if user_ids is not None
                else torch.arange(u_lo, u_hi, device=user_table.device))
         if sample_thr is not None:

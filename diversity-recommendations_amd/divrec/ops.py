@@ -384,29 +384,6 @@ def ild_labels(recs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
 
 
 _KINDS = {"cosine": B.DR_ILD_COSINE, "dot": B.DR_ILD_DOT, "euclidean": B.DR_ILD_EUCLIDEAN}
-_PAD_CACHE: list = []  # [(weakref to the source tensor, its version, width, padded copy)]
-
-
-def pad_columns_cached(table: torch.Tensor, width: int) -> torch.Tensor:
-    """pad_columns, reusing the padded copy of the last two tables padded here
-    while the source tensor object is alive and unmodified (its autograd
-    version is unchanged; the fused optimizer steps bump it on raw-pointer
-    writes). ILD and MMR are called repeatedly on one item table (the
-    reference experiments' d = 100 has no kernel instance), so the multi-GB
-    copy of a 10M-row catalog is made once, not per call."""
-    import weakref
-
-    if table.size(1) == width:
-        return table
-    for ref, ver, w, out in _PAD_CACHE:
-        if ref() is table and ver == table._version and w == width:
-            return out
-    out = pad_columns(table, width)
-    _PAD_CACHE.insert(0, (weakref.ref(table), table._version, width, out))
-    del _PAD_CACHE[2:]
-    return out
-
-
 ILD_WIDTHS = (32, 64, 128, 256)  # dr_ild_embedding instances; others are zero-padded
 MMR_WIDTHS = (64, 128)           # dr_mmr_rerank instances; others are zero-padded
 
@@ -428,8 +405,11 @@ def ild_embedding(recs: torch.Tensor, item_table: torch.Tensor, kind: str = "cos
     _need(item_table.dtype == torch.bfloat16 and item_table.dim() == 2, "item_table must be bf16 2-D")
     _contig(item_table, "item_table")
     _need(kind in _KINDS, f"kind must be one of {sorted(_KINDS)}")
-    item_table = pad_columns_cached(item_table,
-                                    _width_of(ILD_WIDTHS, item_table.size(1), "embedding ILD"))
+    # a width without a kernel instance (e.g. d = 100) is zero-padded per call,
+    # never cached: writes through .data or raw pointers bump no version a
+    # cache could key on. Repeated callers pad once themselves
+    # (EmbeddingDistance holds its padded table; pad_columns is public).
+    item_table = pad_columns(item_table, _width_of(ILD_WIDTHS, item_table.size(1), "embedding ILD"))
     n, k = recs.shape
     _need(k <= 16384, "embedding ILD supports k <= 16384")
     out = torch.empty(n, dtype=torch.float32, device=dev)
@@ -588,15 +568,15 @@ def mmr_rerank(
     Candidate ids < 0 are empty slots; with ``check`` an id >= the table's row
     count raises IndexError after the call (one counter read), as indexing the
     table would (without it such candidates are silently never picked).
-    Widths other than 64 / 128 are zero-padded here, once per table version
-    (pad_columns_cached)."""
+    Widths other than 64 / 128 are zero-padded per call (no cache, so every
+    write to the table is seen; pass a pre-padded table to avoid the copy)."""
     dev = B.require_device(cand_items, cand_scores, item_table)
     _need(cand_items.dtype == torch.int32 and cand_scores.dtype == torch.float32,
           "int32 candidate ids, fp32 scores")
     _need(cand_items.dim() == 2 and cand_items.shape == cand_scores.shape, "[n, C] inputs")
     _need(item_table.dtype == torch.bfloat16 and item_table.dim() == 2, "item_table must be bf16 2-D")
-    item_table = pad_columns_cached(item_table.contiguous(),
-                                    _width_of(MMR_WIDTHS, item_table.size(1), "mmr_rerank"))
+    item_table = pad_columns(item_table.contiguous(),
+                             _width_of(MMR_WIDTHS, item_table.size(1), "mmr_rerank"))
     n, C = cand_items.shape
     out = torch.empty((n, int(k_out)), dtype=torch.int32, device=dev)
     if n == 0:

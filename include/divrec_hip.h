@@ -51,6 +51,27 @@ const char* dr_build_id(void);
 /* Thread-local message of the last failing call on this thread ("" if none). */
 const char* dr_last_error(void);
 
+/* Planner knobs: process-wide overrides of dr_score_topk's launch planner (and
+ * of dr_mmr_rerank's grid, DR_KNOB_SCAN_SLOTS), for tests and A/B timing runs
+ * only. Every plan gives identical results; only the time differs. The
+ * library reads no environment variable: a knob holds the default plan until
+ * it is set here, and value NaN restores the default. Thread-safe (atomic). */
+enum dr_plan_knob {
+  DR_KNOB_SCAN_SLOTS = 0,   /* workgroup slots planned for (split-tail plans at small sizes) */
+  DR_KNOB_SCAN_SPLIT = 1,   /* max catalog chunks of a tail block (1 = no split) */
+  DR_KNOB_TAIL_KEYS = 2,    /* finalize key cap of a split-tail user */
+  DR_KNOB_SCAN_SEED = 3,    /* 0: never seed from a sample; 1: always (>= 2^18 rows) */
+  DR_KNOB_GUESS_STRIDE = 4, /* sample stride of the guessed thresholds */
+  DR_KNOB_GUESS_Z1 = 5,     /* first-tier margin z (ks1 = mu + z sigma + c1) */
+  DR_KNOB_GUESS_C1 = 6,     /* first-tier offset c1 */
+  DR_KNOB_GUESS_TIGHT = 7,  /* 0: one tier (ks1 = ks) */
+  DR_KNOB_COUNT = 8
+};
+/* Set knob `knob` to `value` (NaN = default). DR_EINVAL for an unknown knob. */
+int dr_set_plan_knob(int knob, double value);
+/* Current value of a knob (NaN = default; NaN for an unknown knob). */
+double dr_get_plan_knob(int knob);
+
 /* ---------------------------------------------------------------------------
  * Id range checks (all gather-type calls below): an id outside [0, rows) of
  * its table — what nn.Embedding / tensor indexing reject with IndexError in
@@ -119,8 +140,7 @@ int dr_score_topk(const void* user_table, const int64_t* user_ids, int64_t n_use
                   size_t workspace_bytes, dr_stream_t stream);
 
 /* The launch plan dr_score_topk uses for these arguments on the current device
- * (host-only query, no device work; planner knobs DIVREC_SCAN_SLOTS /
- * DIVREC_SCAN_SPLIT / DIVREC_TAIL_KEYS / DIVREC_SCAN_SEED / DIVREC_GUESS_STRIDE
+ * (host-only query, no device work; the planner knobs of dr_set_plan_knob
  * included), so tests can show which plan they exercised. out[0..11] = users per
  * workgroup, user blocks, head blocks (scanned whole), catalog chunks per tail
  * block (1 = no split), tail chunk length, grid, candidate capacity, sample

@@ -300,24 +300,11 @@ def test_score_topk_guess_rescan_many_units_exact(d):
     assert np.array_equal(s.cpu().numpy(), ref_s)
 
 
-class _Slots:
-    """Workgroup-slot count the scan planner plans for (DIVREC_SCAN_SLOTS):
-    small counts reach the split-tail plans with small inputs."""
-
-    def __init__(self, n):
-        self.n = n
-
-    def __enter__(self):
-        import os
-        self.old = os.environ.get("DIVREC_SCAN_SLOTS")
-        os.environ["DIVREC_SCAN_SLOTS"] = str(self.n)
-
-    def __exit__(self, *exc):
-        import os
-        if self.old is None:
-            os.environ.pop("DIVREC_SCAN_SLOTS", None)
-        else:
-            os.environ["DIVREC_SCAN_SLOTS"] = self.old
+def _Slots(n):
+    """Workgroup-slot count the scan planner plans for (the scan_slots knob,
+    dr_set_plan_knob): small counts reach the split-tail plans with small inputs."""
+    from divrec import _backend
+    return _backend.plan_knobs(scan_slots=n)
 
 
 def _exact_topk_torch_excl(U, I, k, frozen, block=256):
@@ -989,24 +976,33 @@ def test_mmr_rerank_persistent_prefetch_short_lists(d, C):
     assert all(sorted(got[u].tolist()) == sorted(cand[u].tolist()) for u in users)
 
 
-def test_padded_item_table_cached_per_version():
+def test_padded_item_table_sees_data_writes():
     """ILD / MMR on a width without a kernel instance (d = 100) pad the item
-    table once per table version: repeated calls reuse the
-    padded copy, an in-place update of the table is seen."""
+    table per call, with no cache: writes through ``.data`` (which
+    bump no autograd version) and in-place updates are always seen, like
+    score_topk's (test_score_topk_sees_data_writes)."""
     rng = np.random.default_rng(100)
     ni, d, n, k = 3000, 100, 50, 10
     E = torch.from_numpy(rng.standard_normal((ni, d)).astype(np.float32)).to(DEV).to(torch.bfloat16)
     recs = torch.from_numpy(rng.integers(0, ni, (n, k))).to(DEV)
-    a = ops.ild_embedding(recs, E)
-    p1 = ops.pad_columns_cached(E, 128)
-    b = ops.ild_embedding(recs, E)
-    assert ops.pad_columns_cached(E, 128) is p1 and torch.equal(a, b)
-    ref = ops.ild_embedding(recs, ops.pad_columns(E, 128))
-    assert torch.equal(a, ref)
-    E.mul_(2.0)  # version bump: a fresh padded copy (cosine unchanged, dot x4)
-    assert ops.pad_columns_cached(E, 128) is not p1
-    assert torch.allclose(ops.ild_embedding(recs, E, "dot"), 4 * ops.ild_embedding(recs, p1, "dot"),
-                          rtol=1e-5)
+    a = ops.ild_embedding(recs, E, "dot")
+    assert torch.equal(a, ops.ild_embedding(recs, ops.pad_columns(E, 128), "dot"))
+    ver = E._version
+    E.data.mul_(2.0)  # no version bump
+    assert E._version == ver
+    assert torch.allclose(ops.ild_embedding(recs, E, "dot"), 4 * a, rtol=1e-5)
+    # MMR at lambda = 0 (pure diversity) on the padded table: the picks follow
+    # the rows, so a .data write that swaps two candidates' rows changes them
+    C = 64
+    torch.manual_seed(7)
+    cand = torch.stack([torch.randperm(ni, device=DEV)[:C] for _ in range(n)]).to(torch.int32)
+    sc = torch.sort(torch.rand(n, C, device=DEV), dim=1, descending=True).values
+    p1 = ops.mmr_rerank(cand, sc, E, 8, 0.0)
+    assert torch.equal(p1, ops.mmr_rerank(cand, sc, ops.pad_columns(E, 128), 8, 0.0))
+    E.data[cand[:, 1].long()] = E.data[cand[:, 0].long()]  # candidate 1 duplicates candidate 0
+    p2 = ops.mmr_rerank(cand, sc, E, 8, 0.0)
+    assert torch.equal(p2, ops.mmr_rerank(cand, sc, ops.pad_columns(E, 128), 8, 0.0))
+    assert not torch.equal(p1, p2)
 
 
 @pytest.mark.parametrize("d,n_sample,ks1,ks,ids", [(128, 78125, 5, 10, False), (64, 31250, 10, 17, True),
@@ -1069,6 +1065,36 @@ def test_ild_embedding_long_lists(d, k, kind):
     assert np.isnan(out[3]) and np.allclose(np.delete(out, 3), np.delete(got, 3))
     with pytest.raises(IndexError):
         ops.ild_embedding(torch.from_numpy(bad).to(DEV), _bf16(E), kind)
+
+
+@pytest.mark.parametrize("kind", ["cosine", "dot", "euclidean"])
+def test_ild_embedding_longest_lists(kind):
+    """The advertised upper bound, k = 16384 (64 KB of per-row terms in the
+    dynamically sized LDS array), and k = 16383 (a partial last tile), at
+    d = 32 against a float64 restatement of the reference's pair sum
+    (divrec/losses/intra_list_diversity_score.py:36-42) on the device."""
+    rng = np.random.default_rng(16384)
+    ni, d = 20000, 32
+    E = oracle.as_bf16_f32(rng.standard_normal((ni, d)).astype(np.float32))
+    Et = torch.from_numpy(E).to(DEV).double()
+    for k in (16384, 16383):
+        recs = rng.integers(0, ni, size=(2, k))
+        got = ops.ild_embedding(torch.from_numpy(recs).to(DEV), _bf16(E), kind).cpu().numpy()
+        for u in range(2):
+            x = Et[torch.from_numpy(recs[u]).to(DEV)]
+            g = x @ x.t()
+            if kind == "cosine":
+                n = g.diagonal().sqrt()
+                dist = 1.0 - g / (n[:, None] * n[None, :])
+            elif kind == "dot":
+                dist = g
+            else:
+                sq = g.diagonal()
+                dist = (sq[:, None] + sq[None, :] - 2.0 * g).clamp_min(0.0).sqrt()
+            ref = (dist.triu(1).sum() / (k * (k - 1))).item()
+            scale = dist.abs().mean().item()
+            assert abs(got[u] - ref) <= 2e-5 * max(abs(ref), scale), (k, u, got[u], ref)
+            del g, dist
 
 
 @pytest.mark.parametrize("k", [1025, 3000])

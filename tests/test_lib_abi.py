@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "divrec_hip.h")
 
 def declared_functions():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(dr_\w+)\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|double|const char\*)\s+(dr_\w+)\(", text, re.M)))
 
 
 def test_header_declares_all_bound_symbols():
@@ -129,27 +129,55 @@ def test_ops_fail_loudly_without_gpu():
         ops.gather_dot(t, t, torch.zeros(2, dtype=torch.int64), torch.zeros(2, dtype=torch.int64))
 
 
-def test_workspace_reflects_split_tail_plan(monkeypatch):
+def test_workspace_reflects_split_tail_plan():
     """The planner (host only) splits the grid tail: 1M users at d=128 are 977
     user blocks for 256 workgroup slots, so 768 blocks scan the 10M catalog
     whole and each of the 209 tail blocks is split into 6 chunks, whose extra
     candidate buffers (5 x 209 x 1024 rows of CAP 512 keys) the workspace
-    holds; with the split off (DIVREC_SCAN_SPLIT=1) only one buffer per user
+    holds; with the split off (scan_split = 1) only one buffer per user
     remains (DESIGN.md §3.1 grid tail)."""
     lib = _backend.load_library()
     bf16 = _backend.DR_BF16
-    monkeypatch.setenv("DIVREC_SCAN_SLOTS", "256")
     one = (1_000_000 + 448) * 512 * 8  # padded users x CAP x 8 B
     extra = 5 * 209 * 1024 * 512 * 8
-    split = lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100)
-    assert one + extra <= split < one + extra + 200_000_000
+    with _backend.plan_knobs(scan_slots=256):
+        split = lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100)
+        assert one + extra <= split < one + extra + 200_000_000
+        with _backend.plan_knobs(scan_split=1):
+            whole = lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100)
+        assert one <= whole < one + 100_000_000
+        # a grid of exactly one full round has no tail to split
+        full = lib.dr_score_topk_workspace(256 * 1024, 10_000_000, bf16, 128, 100)
+        assert full < 256 * 1024 * 512 * 8 + 100_000_000
+
+
+def test_plan_knobs_set_restore_and_no_environment(monkeypatch):
+    """The planner knobs live in the library (dr_set_plan_knob), NaN = default;
+    plan_knobs restores the previous values; environment variables of the
+    round-4 knob names change nothing (the product reads no environment)."""
+    import math
+    lib = _backend.load_library()
+    bf16 = _backend.DR_BF16
+    assert all(math.isnan(lib.dr_get_plan_knob(i)) for i in range(8))
+    assert lib.dr_set_plan_knob(8, 1.0) == -1  # DR_EINVAL: unknown knob
+    out = (ctypes.c_int64 * 13)()
+    assert lib.dr_score_topk_plan(1_000_000, 10_000_000, bf16, 128, 100, out, 13) == 0
+    base = list(out)
+    monkeypatch.setenv("DIVREC_GUESS_STRIDE", "64")
     monkeypatch.setenv("DIVREC_SCAN_SPLIT", "1")
-    whole = lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100)
-    assert one <= whole < one + 100_000_000
-    # a grid of exactly one full round has no tail to split
-    monkeypatch.delenv("DIVREC_SCAN_SPLIT")
-    full = lib.dr_score_topk_workspace(256 * 1024, 10_000_000, bf16, 128, 100)
-    assert full < 256 * 1024 * 512 * 8 + 100_000_000
+    assert lib.dr_score_topk_plan(1_000_000, 10_000_000, bf16, 128, 100, out, 13) == 0
+    assert list(out) == base
+    with _backend.plan_knobs(scan_split=1):  # no split: the 10M catalog is then not seeded
+        assert lib.dr_score_topk_plan(1_000_000, 10_000_000, bf16, 128, 100, out, 13) == 0
+        assert out[3] == 1 and out[7] == 0 and base[3] > 1 and base[7] == 128
+    with _backend.plan_knobs(guess_stride=64):
+        assert lib.dr_get_plan_knob(4) == 64.0
+        assert lib.dr_score_topk_plan(1_000_000, 10_000_000, bf16, 128, 100, out, 13) == 0
+        assert out[7] == 64
+    assert math.isnan(lib.dr_get_plan_knob(4)) and math.isnan(lib.dr_get_plan_knob(1))
+    with pytest.raises(ValueError):
+        with _backend.plan_knobs(no_such_knob=1):
+            pass
 
 
 def test_seeded_topk_argument_errors_and_workspace():

@@ -18,8 +18,8 @@ Integer-valued tables make every score an exact integer in fp32 (|score| <=
 computed in float64 on the device (exact for these integers) and ranked by a
 stable descending sort over ascending item ids, which is the key order.
 
-* small shapes, planner knobs: DIVREC_GUESS_STRIDE 64 / 128 with
-  DIVREC_SCAN_SLOTS split plans, exclusions, duplicate user ids and "hot"
+* small shapes, planner knobs (dr_set_plan_knob): guess_stride 64 / 128 with
+  scan_slots split plans, exclusions, duplicate user ids and "hot"
   sample rows that make the guess fail for a user group (device-counted
   rescan);
 * full size: 1M x 10M d = 128 k = 100 and 1M x 1M d = 64 k = 100, the calls
@@ -40,23 +40,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-class _Env:
-    """Set planner knobs (environment variables read at each dr_score_topk call)."""
-
-    def __init__(self, **kv):
-        self.kv = {k: str(v) for k, v in kv.items() if v is not None}
-
-    def __enter__(self):
-        self.old = {k: os.environ.get(k) for k in self.kv}
-        os.environ.update(self.kv)
-        return self
-
-    def __exit__(self, *exc):
-        for k, v in self.old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+def _Env(**kv):
+    """Set planner knobs (dr_set_plan_knob, through divrec._backend.plan_knobs)
+    for a block; None leaves a knob at its default."""
+    from divrec import _backend
+    return _backend.plan_knobs(**{k: v for k, v in kv.items() if v is not None})
 
 
 def exact_topk_f64(U64: torch.Tensor, I64: torch.Tensor, k: int, frozen=None, block: int = 16):
@@ -129,7 +117,7 @@ def test_forced_stride_split_rescan_exact(d, stride, slots):
         frozen[n] = np.union1d(frozen[n], np.concatenate([best, [stride * 3]]))
     rowptr, cols = oracle.exclusion_csr(frozen)
     Ub, Ib = torch.from_numpy(U).to(DEV).to(torch.bfloat16), torch.from_numpy(I).to(DEV).to(torch.bfloat16)
-    with _Env(DIVREC_GUESS_STRIDE=stride, DIVREC_SCAN_SLOTS=slots):
+    with _Env(guess_stride=stride, scan_slots=slots):
         plan = ops.score_topk_plan(len(users), ni, torch.bfloat16, d, k)
         s, it = ops.score_topk(Ub, Ib, k, user_ids=torch.from_numpy(users).to(DEV),
                                exclude=(torch.from_numpy(rowptr).to(DEV),
@@ -149,7 +137,7 @@ def test_forced_stride_k1000_split():
     U = rng.integers(-3, 4, size=(nu, d)).astype(np.float32)
     I = rng.integers(-3, 4, size=(ni, d)).astype(np.float32)
     Ub, Ib = torch.from_numpy(U).to(DEV).to(torch.bfloat16), torch.from_numpy(I).to(DEV).to(torch.bfloat16)
-    with _Env(DIVREC_GUESS_STRIDE=64, DIVREC_SCAN_SLOTS=3):  # 4 blocks: 3 head + a split tail
+    with _Env(guess_stride=64, scan_slots=3):  # 4 blocks: 3 head + a split tail
         plan = ops.score_topk_plan(nu, ni, torch.bfloat16, d, k)
         s, it = ops.score_topk(Ub, Ib, k)
     assert plan["sample_stride"] == 64 and plan["tail_chunks"] == 2
@@ -161,7 +149,7 @@ def test_forced_stride_k1000_split():
                                     (128, 100, 5 * 1024 + 1)])
 def test_second_tier_every_user_exact(d, k, nu):
     """The two-tier guess with the first tier forced almost useless
-    (DIVREC_GUESS_Z1=-5: the main scan starts from the sample's best score or
+    (guess_z1 = -5: the main scan starts from the sample's best score or
     so): nearly every user fails the first tier and is recomputed by the
     second tier, whose device-side plan splits the many failing blocks over
     the grid and whose streaming finalize merges any number of keys per user
@@ -177,7 +165,7 @@ def test_second_tier_every_user_exact(d, k, nu):
     rowptr, cols = oracle.exclusion_csr(frozen)
     Ub, Ib = torch.from_numpy(U).to(DEV).to(torch.bfloat16), torch.from_numpy(I).to(DEV).to(torch.bfloat16)
     st = {}
-    with _Env(DIVREC_GUESS_Z1=-5):
+    with _Env(guess_z1=-5):
         s, it = ops.score_topk(Ub, Ib, k, exclude=(torch.from_numpy(rowptr).to(DEV),
                                                    torch.from_numpy(cols).to(DEV)), stats=st)
     t1, t2 = st["guess_failures"]

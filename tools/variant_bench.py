@@ -5,8 +5,10 @@
 
 Each entry of --libs is a library tag: "product" is divrec/_lib/libdivrec_hip.so,
 any other tag T is divrec/_lib/libdivrec_hip_T.so. A tag may carry planner
-knobs read from the environment at each call, "product@DIVREC_SCAN_SPLIT=1"
-(several joined by "+"): the same library timed under another plan. Every library is loaded into
+knobs, "product@scan_split=1" (several joined by "+"; names of
+divrec._backend.PLAN_KNOBS, set through dr_set_plan_knob before each call;
+round-4 libraries, which read DIVREC_<NAME> environment variables instead, get
+those too): the same library timed under another plan. Every library is loaded into
 this one process (separate code objects), fed the same device inputs, and timed
 with HIP events on the current stream, round-robin, `--rounds` times. The
 outputs of every build must equal the first build's bit for bit (the ranking
@@ -50,7 +52,10 @@ def lib_for(tag):
     sigs = dict(B.SIGNATURES)
     if tag.startswith("abi1"):
         sigs.update(_ABI1)
-    for fn in ("dr_score_topk_workspace", "dr_score_topk", "dr_last_error", "dr_mmr_rerank"):
+    for fn in ("dr_score_topk_workspace", "dr_score_topk", "dr_last_error", "dr_mmr_rerank",
+               "dr_set_plan_knob"):
+        if not hasattr(lib, fn):
+            continue  # libraries from before the knob ABI
         res, args = sigs[fn]
         f = getattr(lib, fn)
         f.restype, f.argtypes = res, args
@@ -80,10 +85,12 @@ def main():
 
     def run(t):
         L = libs[t]
-        for key in ("DIVREC_SCAN_SPLIT", "DIVREC_SCAN_SEED", "DIVREC_SCAN_SLOTS", "DIVREC_GUESS_STRIDE",
-                    "DIVREC_TAIL_KEYS", "DIVREC_GUESS_TIGHT", "DIVREC_GUESS_Z1", "DIVREC_GUESS_C1"):
-            os.environ.pop(key, None)
-        os.environ.update(envs[t])
+        knobs = {k.lower().replace("divrec_", ""): v for k, v in envs[t].items()}
+        for name, i in B.PLAN_KNOBS.items():
+            os.environ.pop("DIVREC_" + name.upper(), None)
+            if hasattr(L, "dr_set_plan_knob"):
+                L.dr_set_plan_knob(i, float(knobs[name]) if name in knobs else float("nan"))
+        os.environ.update({"DIVREC_" + k.upper(): v for k, v in knobs.items()})
         dt = () if t.startswith("abi1") else (B.DR_BF16,)
         ws_bytes = L.dr_score_topk_workspace(args.users, args.items, *dt, d, args.k)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
