@@ -602,6 +602,7 @@ struct TopkArgs {
   int tail_chunks;
   int64_t chunk_items;  // multiple of the stage's item count
   int end_keep;         // tail chunk units compact buffers above this count at their end
+  int head_keep;        // whole-catalog units compact buffers above this count at their end (0: none)
   int slack;            // keys a compaction keeps beyond k (kSlack; smaller for sample scans)
   int gap;              // new keys a buffer takes past k + slack before it is compacted
   const float* init_thr;  // [n_users_pad] starting thresholds (SEEDED scans only)
@@ -770,7 +771,8 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
     const int64_t brow0 = brow + (int64_t)wave * UPW;      // its first buffer row
     // the unit's last compaction test: a chunk of a split tail block keeps at
     // most end_keep keys per user, so the finalize gathers a bounded count
-    const int last_lim = (chunked && a.end_keep > 0 && a.end_keep < flush_at) ? a.end_keep : flush_at;
+    const int keep = chunked ? a.end_keep : a.head_keep;
+    const int last_lim = (keep > 0 && keep < flush_at) ? keep : flush_at;
     uint64_t* cbase = a.cand + (size_t)brow0 * CAP;
 
     // Resident B fragments: lane holds user (ut*32+col), k = 16s + 8h .. +7.
@@ -1243,7 +1245,8 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
       }
     }
     }
-    // a chunk of a split tail block ends with at most end_keep keys per user
+    // a chunk of a split tail block ends with at most end_keep keys per user,
+    // a whole-catalog unit of a long-list plan with at most head_keep
     if (last_lim < flush_at && ntiles > 0) check_compact(last_lim, last_lim - a.k);
     wait_vmcnt<0>();
     wave_lds_sync();
@@ -1271,6 +1274,7 @@ struct Plan {
   int tail_chunks;      // catalog chunks per tail block (1 = no split)
   int64_t chunk_items;  // tail chunk length
   int end_keep;         // keys a tail chunk buffer keeps at its end (0: no end compaction)
+  int head_keep;        // keys a whole-catalog buffer keeps at its end (0: no end compaction)
   int slack, gap;       // compaction slack and flush gap (TopkArgs)
   int64_t buf_rows;     // candidate buffers: n_users_pad + the tail's extra chunks
   int grid;

@@ -399,6 +399,9 @@ constexpr int kSampleGap = DR_SAMPLE_GAP;
 // (<= k + kSlack each) in one wave; at most 1024 of them keeps its sort at
 // P = 16 (a 2048-key sort costs ~6x the 512-key one of a whole-catalog user).
 constexpr int kMaxTailKeys = 1024;
+#ifndef DR_HEAD_KEEP
+#define DR_HEAD_KEEP 1  // long lists: whole-catalog units end compacted to 1024 keys (0: A/B off)
+#endif
 
 // Grid tail: U users make B = ceil(U / UPWG) user blocks for `slots`
 // workgroups. Whole-catalog units run in ceil(B / slots) rounds, the last one
@@ -468,6 +471,11 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   // a tail chunk ends with at most end_keep >= k keys, so c of them fit the
   // finalize's max_keys
   p.end_keep = best_c > 1 ? std::min(k + kSlack, max_keys / best_c) : 0;
+  // Long lists (the flush bound above 1024 keys): every whole-catalog unit ends
+  // with a compaction to at most kMaxTailKeys keys (slack kMaxTailKeys - k), so
+  // the finalize sorts 1024 keys per user instead of 2048 (k = 1000: the
+  // 2048-key sort cost ~24 ms per 1M users).
+  p.head_keep = DR_HEAD_KEEP && head_flush > kMaxTailKeys && k + 8 <= kMaxTailKeys ? kMaxTailKeys : 0;
   p.buf_rows = p.n_users_pad + (int64_t)(best_c - 1) * (B - p.n_head) * p.users_per_wg;
   const int64_t units = p.n_head + (B - p.n_head) * best_c;
   p.grid = (int)(units < slots ? units : slots);
@@ -487,11 +495,12 @@ int flush_keys(const Plan& p, int w, int k) {
   return f < m ? f : m;
 }
 int head_keys(const Plan& p, int w, int k) {
-  const int n = flush_keys(p, w, k);
+  const int n = p.head_keep > 0 ? p.head_keep : flush_keys(p, w, k);
   return n > 256 ? n : 256;
 }
 int tail_keys(const Plan& p, int w, int k) {
-  const int n = p.tail_chunks > 1 ? p.tail_chunks * p.end_keep : flush_keys(p, w, k);
+  if (p.tail_chunks <= 1) return head_keys(p, w, k);
+  const int n = p.tail_chunks * p.end_keep;
   return n > 256 ? n : 256;
 }
 
@@ -832,6 +841,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   a.tail_chunks = p.tail_chunks;
   a.chunk_items = p.chunk_items;
   a.end_keep = p.end_keep;
+  a.head_keep = p.head_keep;
   a.slack = p.slack;
   a.gap = p.gap;
   a.init_thr = nullptr;
@@ -923,6 +933,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   as.tail_chunks = ps.tail_chunks;
   as.chunk_items = ps.chunk_items;
   as.end_keep = ps.end_keep;
+  as.head_keep = ps.head_keep;
   as.slack = ps.slack;
   as.gap = ps.gap;
   as.gmax = DR_SAMPLE_GMAX;
@@ -1097,6 +1108,7 @@ extern "C" int dr_score_topk_seeded(const void* user_table, const int64_t* user_
   a.tail_chunks = p.tail_chunks;
   a.chunk_items = p.chunk_items;
   a.end_keep = p.end_keep;
+  a.head_keep = p.head_keep;
   a.slack = p.slack;
   a.gap = p.gap;
   a.init_thr = init_thr;
@@ -1237,6 +1249,7 @@ extern "C" int dr_sample_thresholds(const void* user_table, const int64_t* user_
   a.tail_chunks = p.tail_chunks;
   a.chunk_items = p.chunk_items;
   a.end_keep = p.end_keep;
+  a.head_keep = p.head_keep;
   a.slack = p.slack;
   a.gap = p.gap;
   a.gmax = 1;

@@ -217,6 +217,10 @@ def test_headline_plans_on_a_256_cu_device():
     assert ops.score_topk_plan(1_000_000, 5_000_000, bf, 128, 100)["sample_stride"] == 64
     p = ops.score_topk_plan(1_000_000, 10_000_000, bf, 128, 1000)
     assert (p["sample_stride"], p["cap"]) == (32, 2048)
+    # long lists: whole-catalog units end compacted to 1024 keys (a 1024-key
+    # finalize instead of 2048); 977 blocks on 256 CUs: no split pays here
+    assert (p["tail_chunks"], p["head_keys"], p["tail_keys"]) == (1, 1024, 1024)
+    assert ops.score_topk_plan(1_000_000, 10_000_000, bf, 128, 100)["head_keys"] == 256
     assert ops.score_topk_plan(1000, 100_000, bf, 128, 100)["sample_stride"] == 0  # plain scan
 
 
