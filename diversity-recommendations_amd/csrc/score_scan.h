@@ -114,8 +114,13 @@ enum {
 #ifndef DR_WAVES
 #define DR_WAVES 8  // 8: two waves per SIMD (256 registers each); 4: one per SIMD (512)
 #endif
-constexpr int kWaves = DR_WAVES;
-constexpr int kThreads = kWaves * 64;
+#ifndef DR_WAVES_NARROW
+#define DR_WAVES_NARROW DR_WAVES  // waves per workgroup for rows of <= 128 bytes (d <= 64 bf16)
+#endif
+// Waves per workgroup of a scan over rows of w bf16 units (one workgroup per
+// CU): the register budget per wave is 512 / (waves / 4) VGPRs.
+constexpr int waves_for(int w) { return w <= 64 ? DR_WAVES_NARROW : DR_WAVES; }
+constexpr int kMaxWaves = DR_WAVES > DR_WAVES_NARROW ? DR_WAVES : DR_WAVES_NARROW;
 // Longest catalog a staged (W <= 64) scan takes: its staged blocks name their
 // tile in 23 bits (dr_score_topk refuses longer ones).
 constexpr int64_t kMaxStagedRows = (int64_t)32 << 23;
@@ -131,19 +136,26 @@ constexpr int kFlushGap = DR_FLUSH_GAP;
 // +6 % at 1.25M, where the survivor stream makes per-stage wave imbalance
 // larger). d <= 64: three 32-KB slots (its LDS survivor staging needs room;
 // 64-KB stages measured -10 % there; d = 256 spills with them).
-constexpr int stage_bytes_for(int w) { return w == 128 ? DR_STAGE_BYTES_WIDE : DR_STAGE_BYTES; }
+#ifndef DR_STAGE_BYTES_NARROW
+#define DR_STAGE_BYTES_NARROW DR_STAGE_BYTES  // ring slot for d <= 64
+#endif
+constexpr int stage_bytes_for(int w) {
+  return w == 128 ? DR_STAGE_BYTES_WIDE : (w <= 64 ? DR_STAGE_BYTES_NARROW : DR_STAGE_BYTES);
+}
 constexpr int ring_for(int w) { return w == 128 ? DR_RING_WIDE : DR_RING; }
 
 template <int D>  // D = W, the row's width in bf16 units (row bytes / 2)
 struct TileGeom {
+  static constexpr int WAVES = waves_for(D);
+  static constexpr int THREADS = WAVES * 64;
   static constexpr int STAGE_BYTES = stage_bytes_for(D);  // one LDS ring slot
   static constexpr int RING = ring_for(D);                // slots (RING - 1 stages in flight)
-  static constexpr int LPT = STAGE_BYTES / 16 / kThreads;  // LDS-DMA per thread per stage
+  static constexpr int LPT = STAGE_BYTES / 16 / THREADS;  // LDS-DMA per thread per stage
   static constexpr int KSTEPS = D / 16;                 // MFMA k-steps per row
   static constexpr int CPR = D / 8;                     // 16-B chunks per row
   static constexpr int TILE_BYTES = kTileItems * D * 2;
   static constexpr int SR = STAGE_BYTES / TILE_BYTES;   // row tiles per stage
-  static_assert(LPT >= 1 && STAGE_BYTES % (16 * kThreads) == 0, "stage geometry");
+  static_assert(LPT >= 1 && STAGE_BYTES % (16 * THREADS) == 0, "stage geometry");
   static_assert(RING >= 2, "ring depth");
   static constexpr int RPB = (2 * D >= 256) ? 1 : 256 / (2 * D);  // rows per 256-B bank row
   static constexpr int SWM = (CPR < 16 ? CPR : 16) - 1;
@@ -255,7 +267,7 @@ __device__ __forceinline__ void issue_stage(const char* __restrict__ I, int64_t 
   const int rmax = left < ROWS - 1 ? (int)left : ROWS - 1;
 #pragma unroll
   for (int j = 0; j < G::LPT; ++j) {
-    const int wave_first = j * kThreads + wave * 64;  // wave-uniform chunk index
+    const int wave_first = j * G::THREADS + wave * 64;  // wave-uniform chunk index
     const int idx = wave_first + lane;
     const int r = idx / G::CPR;
     const int lc = (idx % G::CPR) ^ G::swz(r & 31);
@@ -629,7 +641,7 @@ struct TopkArgs {
   const int64_t* pos_map;
   uint64_t* cand;  // [buffer rows][CAP] keys (unsorted)
   int32_t* cnt;    // [buffer rows] valid keys per buffer
-  uint64_t* diag;  // [gridDim.x * kWaves][kDgSlots] in DR_TOPK_DIAG builds
+  uint64_t* diag;  // [gridDim.x * waves][kDgSlots] in DR_TOPK_DIAG builds
 };
 
 // Chunking of a second-tier rescan, computed where the failing-user count is
@@ -662,7 +674,7 @@ __host__ __device__ inline DevSplit dev_split_plan(int64_t nb, int64_t grid, int
 }
 
 template <int W, int CAP, bool SEEDED, bool F32, bool GMAX = false>
-__global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkArgs a) {
+__global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_scan_kernel(TopkArgs a) {
   static_assert(!(GMAX && SEEDED), "group-max scans are the (unseeded) sample scans");
   constexpr int D = W;  // geometry is by row bytes: an fp32 row of d is a bf16 row of 2d
   using G = TileGeom<D>;
@@ -673,6 +685,7 @@ __global__ __launch_bounds__(kThreads, kWaves / 4) void score_scan_kernel(TopkAr
   constexpr int KS = G::KSTEPS;
   constexpr int SR = G::SR;
   constexpr int UPW = NU_T * 32;      // users per wave
+  constexpr int kWaves = G::WAVES;
   constexpr int UPWG = UPW * kWaves;  // users per workgroup
   constexpr int P = 8;                // keys per lane per compaction chunk (any CAP)
   constexpr int kRing = G::RING;
@@ -1298,9 +1311,11 @@ bool launch_scan_widths(const Plan& p, const TopkArgs& a, int w, bool seeded, hi
     if (done || w != WW) return;
     done = true;
 #define DR_SCAN(CC, SD) \
-  hipLaunchKernelGGL((score_scan_kernel<WW, CC, SD, F32>), dim3(p.grid), dim3(kThreads), 0, s, a)
+  hipLaunchKernelGGL((score_scan_kernel<WW, CC, SD, F32>), dim3(p.grid), dim3(waves_for(WW) * 64), \
+                     0, s, a)
 #define DR_SCAN_GMAX(CC) \
-  hipLaunchKernelGGL((score_scan_kernel<WW, CC, false, F32, true>), dim3(p.grid), dim3(kThreads), \
+  hipLaunchKernelGGL((score_scan_kernel<WW, CC, false, F32, true>), dim3(p.grid),               \
+                     dim3(waves_for(WW) * 64),                                               \
                      0, s, a)
     if (a.gmax && !seeded) {  // sample scans (ks <= ~70 keys: CAP 512, or 1024 at narrow rows)
       if (p.cap == 512) DR_SCAN_GMAX(512);

@@ -425,7 +425,7 @@ constexpr int kMaxTailKeys = 1024;
 Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   Plan p{};
   p.cap = cap_for(w, k);
-  p.users_per_wg = nut_for(w) * 32 * kWaves;
+  p.users_per_wg = nut_for(w) * 32 * waves_for(w);
   p.n_ublocks = dr::ceil_div(n_users, p.users_per_wg);
   p.n_users_pad = p.n_ublocks * p.users_per_wg;
   const int64_t slots = device_cus();
@@ -595,7 +595,7 @@ Guess guess_for(int64_t n_items, int k, bool split_tail) {
 
 size_t diag_bytes() {
 #ifdef DR_TOPK_DIAG
-  return (size_t)device_cus() * kWaves * kDgSlots * sizeof(uint64_t);
+  return (size_t)device_cus() * kMaxWaves * kDgSlots * sizeof(uint64_t);
 #else
   return 0;
 #endif
