@@ -624,15 +624,16 @@ struct TopkArgs {
   // blocks' chunk-0 rows, bounded by buf_blocks user blocks of buffer rows.
   int dev_split;
   int64_t buf_blocks;
-  // Sample scans of the guessed thresholds (the GMAX instantiation): a lane keeps
-  // only the MAX of its 16 scores of a user tile (one key per 16-row group of a
-  // tile) instead of every score above the threshold. The k-th best group max
-  // is a lower bound of the k-th best score (the best k groups' maxima are k
-  // distinct items), so the guessed threshold stays a valid lower bound — it
-  // only drops below the exact sample rank when two of the best k sample
-  // items share a group (~k^2 / (2 S / 16) of users) — while the survivor
-  // stream of a scan from -inf shrinks up to 16-fold. Keys name the group
-  // (tile row base + 4h), not an item: only their scores are read.
+  // Sample scans of the guessed thresholds (the GMAX instantiation): a user
+  // keeps only the MAX of its 32 scores of a tile (one key per tile) instead of
+  // every score above the threshold. The k-th best tile max is a lower bound
+  // of the k-th best score (the best k tiles' maxima are k distinct items), so
+  // the guessed threshold stays a valid lower bound — it only drops below the
+  // exact sample rank when two of the best k sample items share a tile
+  // (~k^2 / (2 S / 32) of users; the tile-transposed sample puts samples T
+  // apart in a tile) — while the survivor stream of a scan from -inf shrinks
+  // up to 32-fold. Keys name the tile (its row base), not an item: only their
+  // scores are read.
   int gmax;
   // Fallback rescan only: the user count lives on the device (n_users and
   // n_ublocks above are its upper bounds), and pos_map[p] is the caller's
@@ -675,7 +676,7 @@ __host__ __device__ inline DevSplit dev_split_plan(int64_t nb, int64_t grid, int
 
 template <int W, int CAP, bool SEEDED, bool F32, bool GMAX = false>
 __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_scan_kernel(TopkArgs a) {
-  static_assert(!(GMAX && SEEDED), "group-max scans are the (unseeded) sample scans");
+  static_assert(!(GMAX && SEEDED), "tile-max scans are the (unseeded) sample scans");
   constexpr int D = W;  // geometry is by row bytes: an fp32 row of d is a bf16 row of 2d
   using G = TileGeom<D>;
   constexpr int NU_T = nut_for(D);
@@ -1108,11 +1109,11 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
       const uint32_t gbase = (uint32_t)(a.item_base + tile0);
 #pragma unroll
       for (int ut = 0; ut < NG; ++ut) {
-        if (hb[ut] == 0ull) continue;
-        float m = hot_max16(acc[ut]);
-        const bool hit = hot(m, thr[g0 + ut]);
-        const uint64_t bal = __ballot(hit);
+        const uint64_t bal = hb[ut];
         if (bal == 0ull) continue;
+        // the lane's hit bit straight from the ballot's SGPR pair (s_and_saveexec
+        // on it; no VALU re-materialisation of the compare)
+        const bool hit = __builtin_amdgcn_inverse_ballot_w64(bal);
         const int n = __popcll(bal);
         if (nblk + n > SB) resolve(IC<0>{});  // rare (a scan's first stages): few registers
         if (hit) {
@@ -1131,26 +1132,45 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
       DG_ADD(kDgEnqueue, t_e);
       DG_CNT(kDgNEnqueue);
     };
-    // Group-max enqueue (GMAX sample scans): one key per hitting lane, the max
-    // of its 16 scores. It is the whole epilogue of such a scan (the max is
-    // its hot test too). A partial last tile (rows past the slice end repeat
-    // the last row) is skipped: leaving sample rows out only lowers the
+    // Group-max enqueue (GMAX sample scans): one key per user and tile, the
+    // max of the tile's 32 scores of the user (the two half-waves' 16-score
+    // maxima merged by v_permlane32_swap). It is the whole epilogue of such a
+    // scan (the max is its hot test too). Lane h = 0 of a user appends its
+    // key; each user's LDS counter has that one writer, so its slot is a plain
+    // read and write (no atomic: one LDS round trip per user-tile group instead
+    // of one atomic per hitting half-wave, which also conflicted between the
+    // two halves of a user). A partial last tile (rows past the slice end
+    // repeat the last row) is skipped: leaving sample rows out only lowers the
     // sample's order statistics, so the guess stays a lower bound.
     auto enqueue_gmax = [&](int t, f32x16 (&acc)[NG], auto GI) {
       constexpr int g0 = decltype(GI)::value * NG;
       DG_T0(t_e);
       const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
       if (i_end - tile0 < kTileItems) return;
+      float m[NG];
+      uint64_t bal[NG];
+      uint64_t any = 0ull;
 #pragma unroll
       for (int ut = 0; ut < NG; ++ut) {
-        float m = max16(acc[ut]);
-        const bool hit = m > thr[g0 + ut];
-        if (__ballot(hit) == 0ull) continue;
-        if (hit) {
+        const float mh = max16(acc[ut]);  // a value (stored): maxNum, NaN scores skipped
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mh), __float_as_uint(mh),
+                                                         false, false);
+        m[ut] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+        bal[ut] = __ballot(h == 0 && m[ut] > thr[g0 + ut]);
+        any |= bal[ut];
+      }
+      if (any == 0ull) return;
+      uint32_t pos[NG];
+#pragma unroll
+      for (int ut = 0; ut < NG; ++ut) pos[ut] = bal[ut] ? ucnt[(g0 + ut) * 32 + col] : 0u;
+      const uint32_t gkey = (uint32_t)(a.item_base + tile0);
+#pragma unroll
+      for (int ut = 0; ut < NG; ++ut) {
+        if (bal[ut] == 0ull) continue;
+        if ((bal[ut] >> lane) & 1ull) {
           const int slot = (g0 + ut) * 32 + col;
-          const uint32_t pos = atomicAdd(&ucnt[slot], 1u);
-          const uint32_t gkey = (uint32_t)(a.item_base + tile0) + 4u * (uint32_t)h;
-          if (pos < (uint32_t)CAP) st64(cbase + (size_t)slot * CAP + pos, dr::make_key(m, gkey));
+          ucnt[slot] = pos[ut] + 1u;
+          if (pos[ut] < (uint32_t)CAP) st64(cbase + (size_t)slot * CAP + pos[ut], dr::make_key(m[ut], gkey));
         }
         vmc += 1;  // the store above issued once (some lane had a key)
       }
@@ -1160,7 +1180,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
     auto epilogue = [&](int t, f32x16 (&acc)[NG], auto GI) {
       // the stage-end work runs after the last group of the tile
       constexpr bool last_group = decltype(GI)::value == NGRP - 1;
-      if constexpr (GMAX) {  // sample scan: group maxima only
+      if constexpr (GMAX) {  // sample scan: tile maxima only
         enqueue_gmax(t, acc, GI);
         if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) check_compact(flush_at, a.slack);
         return;

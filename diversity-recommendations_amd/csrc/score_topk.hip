@@ -391,7 +391,7 @@ constexpr int kMaxTailChunks = 16;
 #define DR_SAMPLE_GAP 96
 #endif
 #ifndef DR_SAMPLE_GMAX
-#define DR_SAMPLE_GMAX 1  // sample scans keep group maxima (TopkArgs::gmax); 0: every survivor
+#define DR_SAMPLE_GMAX 1  // sample scans keep tile maxima (TopkArgs::gmax); 0: every survivor
 #endif
 constexpr int kSampleSlack = DR_SAMPLE_SLACK;
 constexpr int kSampleGap = DR_SAMPLE_GAP;
@@ -650,10 +650,10 @@ Layout make_layout(int64_t n_users, int64_t n_items, int w, int k) {
 
 // Sample rows, tile-transposed: the S = 32 T sample rows j * stride (j < S)
 // are stored so that sample j = q T + r sits in row q of tile r, i.e. output
-// row p = 32 r + q. A 16-row lane group of a tile (the GMAX sample scan keeps
-// one max per group) then holds samples T apart — catalog rows T * stride
-// apart — so items that cluster by id (e.g. ids ordered by popularity) fall
-// into different groups. 16 B per thread.
+// row p = 32 r + q. A tile (the GMAX sample scan keeps one max per user and
+// tile) then holds samples T apart — catalog rows T * stride apart — so items
+// that cluster by id (e.g. ids ordered by popularity) fall into different
+// tiles. 16 B per thread.
 __global__ __launch_bounds__(256) void sample_rows_kernel(const uint4* __restrict__ I,
                                                           int64_t stride, int64_t S, int cpr,
                                                           uint4* __restrict__ out) {

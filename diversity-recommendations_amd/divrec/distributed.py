@@ -238,7 +238,7 @@ def global_thresholds(user_table: torch.Tensor, item_shard: torch.Tensor, lo: in
     users the first tier failed); -inf where the sample is too short.
 
     On the HIP kernels (no ``local_topk`` given) the ranking is
-    dr_sample_thresholds: the single-GPU guess's group-max sample scan, so the
+    dr_sample_thresholds: the single-GPU guess's tile-max sample scan, so the
     thresholds are lower bounds of the sample ranks. An injected
     ``local_topk`` (CPU tests) ranks the exact sample top-ks instead."""
     sample_thr = None

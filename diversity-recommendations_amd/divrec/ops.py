@@ -255,8 +255,8 @@ def sample_thresholds(user_table: torch.Tensor, sample_rows: torch.Tensor, ks1: 
     """The guessed thresholds of the item-sharded top-k (dr_sample_thresholds):
     ``sample_rows`` are the whole catalog's rows at the guess stride; returns
     fp32 [2, n]: strictly below each user's ks1-th (row 0, first tier) and
-    ks-th (row 1, safe tier) best group-max score of the sample (the
-    dr_score_topk guess's group-max sample scan; -inf when there are fewer)."""
+    ks-th (row 1, safe tier) best tile-max score of the sample (the
+    dr_score_topk guess's tile-max sample scan; -inf when there are fewer)."""
     dev = B.require_device(user_table, sample_rows, user_ids)
     _need(user_table.dtype == sample_rows.dtype and user_table.dtype in SCORE_WIDTHS,
           "user table and sample rows must both be bf16 or both fp32")

@@ -162,8 +162,8 @@ int dr_score_topk_fail_counts(const void* workspace, int64_t n_users, int64_t n_
  * dr_score_topk's own guess: sample_rows [n_sample, d] (dtype as the user
  * table) are the whole catalog's rows at the guess stride, gathered from every
  * shard; the whole 32-row tiles of them (n_sample rounded down) are scanned by
- * the group-max sample scan, and thr1[u] / thr2[u] (fp32 [n_users], device)
- * are set strictly below the ks1-th / ks-th best group-max score of user u
+ * the tile-max sample scan, and thr1[u] / thr2[u] (fp32 [n_users], device)
+ * are set strictly below the ks1-th / ks-th best tile-max score of user u
  * (-inf when there are fewer): lower bounds of the user's ks1-th / ks-th best
  * sample score, the first-tier and safe thresholds of
  * divrec.distributed.thresholded_exchange (replaces nothing in the reference:

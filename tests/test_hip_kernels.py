@@ -1011,10 +1011,10 @@ def test_padded_item_table_sees_data_writes():
 def test_sample_thresholds_group_max(d, n_sample, ks1, ks, ids):
     """dr_sample_thresholds (the item-sharded path's guess): the whole 32-row
     tiles of the sample, tile-transposed (sample q T + r -> row q of tile r),
-    one max per 16-row lane group (rows 4h + 8i + j of a tile), thresholds
-    strictly below each user's ks1-th / ks-th best group max (-inf with fewer
-    groups). Integer tables: every score exact, so the thresholds must equal a
-    torch restatement bit for bit, and never exceed the exact sample ranks."""
+    one max per user and tile (its 32 rows), thresholds strictly below each
+    user's ks1-th / ks-th best tile max (-inf with fewer tiles). Integer tables:
+    every score exact, so the thresholds must equal a torch restatement bit for
+    bit, and never exceed the exact sample ranks."""
     from divrec.distributed import threshold_below
 
     rng = np.random.default_rng(d + n_sample + ks)
@@ -1032,11 +1032,10 @@ def test_sample_thresholds_group_max(d, n_sample, ks1, ks, ids):
         T = Sp // 32
         idx = np.array([(p % 32) * T + p // 32 for p in range(Sp)])
         sc = torch.from_numpy(Uq.astype(np.float64) @ Sm[idx].astype(np.float64).T)
-        sc = sc.view(-1, T, 4, 2, 4)  # tile, i, h, j (row = 4h + 8i + j)
-        gm = sc.amax(dim=(2, 4)).reshape(sc.shape[0], 2 * T)
+        gm = sc.view(-1, T, 32).amax(dim=2)  # one max per user and tile
         top = torch.sort(gm, dim=1, descending=True).values
         for row, kk in ((0, ks1), (1, ks)):
-            if 2 * T >= kk:
+            if T >= kk:
                 ref[row] = threshold_below(top[:, kk - 1].float())
         exact = torch.sort(torch.from_numpy(Uq.astype(np.float64) @ Sm.astype(np.float64).T), dim=1,
                            descending=True).values
