@@ -173,6 +173,13 @@ struct TileGeom {
 constexpr int nut_for(int w) {
   return w >= 512 ? 1 : (w >= 256 ? 2 : (w <= 64 ? DR_NUT_NARROW : DR_NUT));
 }
+#ifndef DR_UTPIPE
+// Software-pipelined epilogue per user tile (the main scans; sample scans keep
+// the group epilogue): the MFMA chain of each (item tile, user tile) job goes
+// to one of two accumulators, and the hot test of the previous job runs right
+// after the next job's chain is issued, i.e. under this wave's own MFMAs.
+#define DR_UTPIPE 1
+#endif
 #ifndef DR_PINGPONG
 // Two user-tile groups with one accumulator set EACH, software-pipelined: the
 // epilogue of one group runs while the other group's MFMAs execute (the wave
@@ -188,6 +195,15 @@ template <int V>
 struct IC {
   static constexpr int value = V;
 };
+// f(IC<I>{}), f(IC<I + 1>{}), ..., f(IC<N - 1>{}): compile-time indices for
+// register arrays (a runtime index would put them in scratch)
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(IC<I>{});
+    static_for<I + 1, N>(f);
+  }
+}
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -214,6 +230,11 @@ __device__ __forceinline__ void lds_wait1(u32x4& v) {
 }
 __device__ __forceinline__ void lds_wait0(u32x4& v) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v) : : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lds_waitn(u32x4& v) {
+  static_assert(N >= 0 && N < 16, "lgkmcnt range");
+  asm volatile("s_waitcnt lgkmcnt(%c1)" : "+v"(v) : "i"(N) : "memory");
 }
 
 // s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at their maxima).
@@ -1203,7 +1224,180 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
           check_compact(flush_at, a.slack);
       }
     };
-    if constexpr (DR_PINGPONG && NGRP == 2) {
+    // -------------------------------------------------- per-user-tile pipeline
+    // (DR_UTPIPE, the main scans): a job is one (item tile t, user tile u)
+    // pair, KS k-steps into ONE accumulator (a single accumulation chain of
+    // v_mfma_f32_32x32x16_bf16 issues at full rate). Jobs run t-major; job
+    // (t, u) writes accumulator u % 2, and its hot test runs right after job
+    // (t, u + 1)'s chain is issued, so the test's max3 chain, compare and
+    // ballot issue while this wave's own next MFMAs execute (an MFMA holds the
+    // SIMD's vector issue for 8 of its 32 cycles) instead of after the whole
+    // group's chain has drained. A hit stages / enqueues the job before its
+    // accumulator is reused two jobs later. The tile's A fragments are read
+    // once (KS ds_read_b128 at the tile start) for all its NU_T jobs; the first
+    // chain retires them one k-step at a time.
+    // Rows of <= 128 bytes only: at d = 128 (the headline) it measured +0.4 %
+    // (a chain of 8 k-steps already covers the group's hot test), and the fp32
+    // d = 128 / bf16 d = 256 instances spill in the loop with it.
+    constexpr bool UTP = DR_UTPIPE && !GMAX && NU_T % 2 == 0 && W <= 64;
+    auto read_a = [&](int t, u32x4 (&af)[KS]) {
+      const uint32_t tb = lds_ring + ((t / SR) % kRing) * kStageBytes + (t % SR) * G::TILE_BYTES;
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2) af[s2] = ds_read_b128_asm(tb + a_off(s2));
+    };
+    auto kstep1 = [&](const u32x4& av, const u32x4& bv, f32x16 acc) -> f32x16 {
+      if constexpr (F32) {
+        const dr::f32x4 a4 = __builtin_bit_cast(dr::f32x4, av), b4 = __builtin_bit_cast(dr::f32x4, bv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[j], b4[j], acc, 0, 0, 0);
+        return acc;
+      } else {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, av),
+                                                       __builtin_bit_cast(bf16x8, bv), acc, 0, 0, 0);
+      }
+    };
+    // the tile's first chain: fragment s retired (lgkmcnt(KS - 1 - s), the
+    // fragment named "+v") right before its k-step
+    auto chain_first = [&](u32x4 (&af)[KS], auto UI) -> f32x16 {
+      constexpr int u = decltype(UI)::value;
+      f32x16 acc = f32x16{};
+      static_for<0, KS>([&](auto SI) {
+        constexpr int s2 = decltype(SI)::value;
+        lds_waitn<KS - 1 - s2>(af[s2]);
+        acc = kstep1(af[s2], bfr[u][s2], acc);
+        // keep each wait right before its k-step (hipcc would hoist the waits
+        // together and wait for all but one fragment before the first MFMA)
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      return acc;
+    };
+    auto chain = [&](const u32x4 (&af)[KS], auto UI) -> f32x16 {
+      constexpr int u = decltype(UI)::value;
+      f32x16 acc = f32x16{};
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2) acc = kstep1(af[s2], bfr[u][s2], acc);
+      return acc;
+    };
+    // staged survivors of one job (d <= 64): the hitting lanes' 16 scores
+    auto stage_ut = [&](int t, const f32x16& ac, uint64_t bal, auto UI) {
+      constexpr int u = decltype(UI)::value;
+      DG_T0(t_e);
+      const bool hit = __builtin_amdgcn_inverse_ballot_w64(bal);
+      const int n = __popcll(bal);
+      if (nblk + n > SB) resolve(IC<0>{});  // rare (a scan's first stages): few registers
+      if (hit) {
+        const int i = nblk + lane_prefix(bal);
+        float4* dst = reinterpret_cast<float4*>(blk_val + i * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[q] = make_float4(ac[4 * q], ac[4 * q + 1], ac[4 * q + 2], ac[4 * q + 3]);
+        blk_meta[i] = make_uint2((uint32_t)t | ((uint32_t)(u * 32 + col) << 23) | ((uint32_t)h << 31),
+                                 __float_as_uint(thr[u]));
+      }
+      nblk += n;
+      DG_ADD(kDgEnqueue, t_e);
+      DG_CNT(kDgNEnqueue);
+    };
+    // direct survivors of one job (d >= 128): one key per lane per round
+    auto enqueue_ut = [&](int t, const f32x16& ac, auto UI) {
+      constexpr int u = decltype(UI)::value;
+      DG_T0(t_e);
+      const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
+      const int valid = (int)((i_end - tile0) < kTileItems ? (i_end - tile0) : kTileItems);
+      const uint32_t gbase = (uint32_t)(a.item_base + tile0);
+      uint32_t vmask = 0xffffu;  // rows past the slice end (last tile only)
+      if (valid < kTileItems) {
+        vmask = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) vmask |= ((r & 3) + 8 * (r >> 2) + 4 * h < valid ? 1u : 0u) << r;
+      }
+      uint32_t mask = 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mask |= (ac[r] > thr[u] ? 1u : 0u) << r;
+      mask &= vmask;
+      const int slot = u * 32 + col;
+      uint64_t* ubuf = cbase + (size_t)slot * CAP;
+      // every hitting lane holds ONE survivor (the common case, full tiles):
+      // it is the lane's maximum, stored without a value select
+      if (vmask == 0xffffu && __ballot((mask & (mask - 1u)) != 0u) == 0ull) {
+        if (__ballot(mask != 0u) != 0ull) {
+          const float m = max16(ac);
+          if (mask != 0u) {
+            const int r = __builtin_ctz(mask);
+            const uint32_t pos = atomicAdd(&ucnt[slot], 1u);
+            if (pos < (uint32_t)CAP)
+              st64(ubuf + pos, dr::make_key(m, gbase + (uint32_t)((r & 3) + 8 * (r >> 2) + 4 * h)));
+          }
+          vmc += 1;
+        }
+      } else {
+        while (__ballot(mask != 0u) != 0ull) {
+          const bool has = mask != 0u;
+          const int r = has ? __builtin_ctz(mask) : 0;
+          mask &= mask - 1u;
+          float v = ac[0];
+#pragma unroll
+          for (int q = 1; q < 16; ++q) v = (r == q) ? ac[q] : v;
+          if (has) {
+            const uint32_t pos = atomicAdd(&ucnt[slot], 1u);
+            if (pos < (uint32_t)CAP)
+              st64(ubuf + pos, dr::make_key(v, gbase + (uint32_t)((r & 3) + 8 * (r >> 2) + 4 * h)));
+          }
+          vmc += 1;
+        }
+      }
+      DG_ADD(kDgEnqueue, t_e);
+      DG_CNT(kDgNEnqueue);
+    };
+    auto test_job = [&](int t, const f32x16& ac, auto UI) {
+      constexpr int u = decltype(UI)::value;
+      DG_T0(t_h);
+      const uint64_t bal = __ballot(hot(hot_max16(ac), thr[u]));
+      DG_ADD(kDgHits, t_h);
+      if (bal == 0ull) return;
+      if constexpr (STAGED) stage_ut(t, ac, bal, UI);
+      else enqueue_ut(t, ac, UI);
+    };
+    auto stage_end_utp = [&]() {
+      if constexpr (STAGED) {
+        if (nblk > 0) resolve(IC<DR_RESOLVE_BATCHED>{});
+      }
+      check_compact(flush_at, a.slack);
+    };
+    if constexpr (UTP) {
+      f32x16 acc0, acc1;  // job (t, u) -> acc(u % 2)
+      for (int t = 0; t < ntiles; ++t) {
+        DG_CNT(kDgNTiles);
+        if (t % SR == 0) {
+          // the previous stage's last job, then its stage-end work (every
+          // job of the stage tested: at most MARGIN keys per user since the
+          // last compaction), then the ring boundary
+          if (t > 0) {
+            test_job(t - 1, acc1, IC<NU_T - 1>{});
+            stage_end_utp();
+          }
+          boundary(t / SR);
+        }
+        u32x4 af[KS];
+        read_a(t, af);
+        DG_T0(t_m);
+        acc0 = chain_first(af, IC<0>{});
+        DG_ADD(kDgMma, t_m);
+        if (t % SR != 0) test_job(t - 1, acc1, IC<NU_T - 1>{});
+        static_for<1, NU_T>([&](auto UI) {
+          constexpr int u = decltype(UI)::value;
+          DG_T0(t_m2);
+          if constexpr (u % 2 == 0) acc0 = chain(af, UI);
+          else acc1 = chain(af, UI);
+          DG_ADD(kDgMma, t_m2);
+          if constexpr (u % 2 == 0) test_job(t, acc1, IC<u - 1>{});
+          else test_job(t, acc0, IC<u - 1>{});
+        });
+      }
+      if (ntiles > 0) {
+        test_job(ntiles - 1, acc1, IC<NU_T - 1>{});
+        stage_end_utp();
+      }
+    } else if constexpr (DR_PINGPONG && NGRP == 2) {
       // Ping-pong: tile t's group-0 MFMAs are issued, then group 1's epilogue
       // of tile t-1 runs under them; group 1's MFMAs of tile t are issued,
       // then group 0's epilogue of tile t runs under them. The stage-end work
