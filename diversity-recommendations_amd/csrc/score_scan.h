@@ -1239,7 +1239,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
     // Rows of <= 128 bytes only: at d = 128 (the headline) it measured +0.4 %
     // (a chain of 8 k-steps already covers the group's hot test), and the fp32
     // d = 128 / bf16 d = 256 instances spill in the loop with it.
-    constexpr bool UTP = DR_UTPIPE && !GMAX && NU_T % 2 == 0 && W <= 64;
+    constexpr bool UTP = DR_UTPIPE && NU_T % 2 == 0 && W <= 64;
     auto read_a = [&](int t, u32x4 (&af)[KS]) {
       const uint32_t tb = lds_ring + ((t / SR) % kRing) * kStageBytes + (t % SR) * G::TILE_BYTES;
 #pragma unroll
@@ -1348,8 +1348,35 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
       DG_ADD(kDgEnqueue, t_e);
       DG_CNT(kDgNEnqueue);
     };
+    // the sample scans' job (GMAX): the user's max of the tile's 32 scores
+    // (enqueue_gmax's rule for one user tile)
+    auto gmax_ut = [&](int t, const f32x16& ac, auto UI) {
+      constexpr int u = decltype(UI)::value;
+      const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
+      const float mh = max16(ac);  // a value (stored): maxNum, NaN scores skipped
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mh), __float_as_uint(mh),
+                                                       false, false);
+      const float m = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      const uint64_t bal = __ballot(h == 0 && m > thr[u]);
+      if (bal == 0ull || i_end - tile0 < kTileItems) return;  // a partial last tile is skipped
+      DG_T0(t_e);
+      if (__builtin_amdgcn_inverse_ballot_w64(bal)) {
+        const int slot = u * 32 + col;
+        const uint32_t pos = ucnt[slot];  // one writer per user counter
+        ucnt[slot] = pos + 1u;
+        if (pos < (uint32_t)CAP)
+          st64(cbase + (size_t)slot * CAP + pos, dr::make_key(m, (uint32_t)(a.item_base + tile0)));
+      }
+      vmc += 1;  // the store above issued once (some lane had a key)
+      DG_ADD(kDgEnqueue, t_e);
+      DG_CNT(kDgNEnqueue);
+    };
     auto test_job = [&](int t, const f32x16& ac, auto UI) {
       constexpr int u = decltype(UI)::value;
+      if constexpr (GMAX) {
+        gmax_ut(t, ac, UI);
+        return;
+      }
       DG_T0(t_h);
       const uint64_t bal = __ballot(hot(hot_max16(ac), thr[u]));
       DG_ADD(kDgHits, t_h);
