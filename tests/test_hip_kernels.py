@@ -279,6 +279,36 @@ def _exact_topk_torch(U, I, k, block=256):
     return torch.cat(outi).numpy().astype(np.int64), torch.cat(outs).numpy()
 
 
+@pytest.mark.parametrize("d", [32, 64, 128])
+def test_score_topk_nan_rows_never_ranked(d):
+    """Item rows holding NaN (a NaN score for every user): the hot test's
+    maximum propagates NaN and counts it as a hit, the exact per-score tests
+    behind it never admit a NaN score, so NaN items are never recommended and
+    every other list is the exact top-k of the finite items (round 5; the
+    round-4 maxNum test skipped NaN the same way). The reference would sort
+    NaN scores with argsort (divrec/train/utils.py:73): a documented
+    divergence. 300K rows: the guessed-threshold path,
+    with NaN rows at sample positions too."""
+    rng = np.random.default_rng(300 + d)
+    nu, ni, k = 3000, 300_011, 50
+    U = _int_table(rng, nu, d)
+    I = _int_table(rng, ni, d)
+    bad = np.unique(np.concatenate([np.arange(0, 40) * 32, rng.choice(ni, 200, replace=False)]))
+    I[bad, d // 2] = np.nan
+    s, it = ops.score_topk(_bf16(U), _bf16(I), k)
+    it = it.cpu().numpy().astype(np.int64)
+    assert not np.isin(it, bad).any()
+    Ifin = I.copy()
+    Ifin[bad] = 0.0
+    ref_i, ref_s = _exact_topk_torch(U, Ifin, k + len(bad))
+    # the finite items' order: drop the zeroed NaN rows from the exact lists
+    keep = ~np.isin(ref_i, bad)
+    exp_i = np.stack([r[m][:k] for r, m in zip(ref_i, keep)])
+    exp_s = np.stack([r[m][:k] for r, m in zip(ref_s, keep)])
+    assert np.array_equal(it, exp_i)
+    assert np.array_equal(s.cpu().numpy(), exp_s)
+
+
 @pytest.mark.parametrize("d", [64, 128])
 def test_score_topk_guess_rescan_many_units_exact(d):
     """Every user fails the guess (hot sampled rows) and there are more of
