@@ -14,6 +14,7 @@ O=gpurun_out/r05reh
 mkdir -p $O
 timeout -k 10 500 python3 bench.py --gpus 8 --backend gloo --same-device --check-users 1024 --steps 1 --warmup 0 --no-cpu-baseline > $O/catalog8.jsonl 2> $O/catalog8.err
 timeout -k 10 400 python3 bench.py --workload mmr --gpus 2 --backend gloo --same-device --users 262144 --steps 1 --warmup 0 --no-cpu-baseline > $O/mmr2.jsonl 2> $O/mmr2.err
+cp gpurun_out/pmck/pmc_*.json gpurun_out/pmcm/pmc_mfma_*.json profiles/
 O=gpurun_out/r05fc
 mkdir -p $O
 timeout -k 10 300 python3 bench.py > $O/bench.jsonl 2> $O/bench.err
