@@ -12,8 +12,8 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 // Knob values, NaN = the default plan. Set only through dr_set_plan_knob: the
 // library reads no environment variable.
 static std::atomic<double> g_knobs[DR_KNOB_COUNT] = {
-    {NAN}, {NAN}, {NAN}, {NAN}, {NAN}, {NAN}, {NAN}, {NAN}};
-static_assert(DR_KNOB_COUNT == 8, "initialise every knob");
+    {NAN}, {NAN}, {NAN}, {NAN}, {NAN}, {NAN}, {NAN}, {NAN}, {NAN}};
+static_assert(DR_KNOB_COUNT == 9, "initialise every knob");
 bool plan_knob(int id, double* v) {
   if (id < 0 || id >= DR_KNOB_COUNT) return false;
   const double x = g_knobs[id].load(std::memory_order_relaxed);

@@ -655,7 +655,16 @@ struct TopkArgs {
   // apart in a tile) — while the survivor stream of a scan from -inf shrinks
   // up to 32-fold. Keys name the tile (its row base), not an item: only their
   // scores are read.
+  //   gmax == 2 (dense tile maxima, ks <= kDenseMaxKs): no keys, no
+  //   counters, no compaction: every (user, tile) maximum is stored to
+  //   tmax[(user / 32) * tmax_tiles + tile][user % 32] (one 128-B line per
+  //   job), and topk_threshold_dense_kernel ranks each user's column. The
+  //   compaction path paid one serialized buffer round trip per user when
+  //   every user's buffer filled in the same stage (the whole workgroup
+  //   waits at the next ring barrier).
   int gmax;
+  float* tmax;
+  int64_t tmax_tiles;
   // Fallback rescan only: the user count lives on the device (n_users and
   // n_ublocks above are its upper bounds), and pos_map[p] is the caller's
   // position of list entry p (its exclusion row). NULL otherwise.
@@ -809,6 +818,14 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
     const int keep = chunked ? a.end_keep : a.head_keep;
     const int last_lim = (keep > 0 && keep < flush_at) ? keep : flush_at;
     uint64_t* cbase = a.cand + (size_t)brow0 * CAP;
+    // dense tile maxima (gmax == 2): the 32 floats of user tile u, tile t of
+    // the unit (unit slices start on tile boundaries; a partial tile's rows
+    // past the slice end repeat its last row, so its max is still one of its
+    // own items' scores)
+    auto dense_tmax = [&](int u, int t) -> float* {
+      return a.tmax + ((size_t)((upos0 >> 5) + u) * (size_t)a.tmax_tiles +
+                       (size_t)((i_beg >> 5) + t)) * 32;
+    };
 
     // Resident B fragments: lane holds user (ut*32+col), k = 16s + 8h .. +7.
     u32x4 bfr[NU_T][KS];  // bf16x8 (bf16 tables) or f32x4 (fp32 tables) per k-step
@@ -1167,7 +1184,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
       constexpr int g0 = decltype(GI)::value * NG;
       DG_T0(t_e);
       const int64_t tile0 = i_beg + (int64_t)t * kTileItems;
-      if (i_end - tile0 < kTileItems) return;
+      if (a.gmax != 2 && i_end - tile0 < kTileItems) return;
       float m[NG];
       uint64_t bal[NG];
       uint64_t any = 0ull;
@@ -1177,9 +1194,15 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
         const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mh), __float_as_uint(mh),
                                                          false, false);
         m[ut] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+        if (a.gmax == 2) {  // dense tile maxima
+          if (h == 0) dense_tmax(g0 + ut, t)[col] = m[ut];
+          vmc += 1;
+          continue;
+        }
         bal[ut] = __ballot(h == 0 && m[ut] > thr[g0 + ut]);
         any |= bal[ut];
       }
+      if (a.gmax == 2) return;
       if (any == 0ull) return;
       uint32_t pos[NG];
 #pragma unroll
@@ -1203,7 +1226,8 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
       constexpr bool last_group = decltype(GI)::value == NGRP - 1;
       if constexpr (GMAX) {  // sample scan: tile maxima only
         enqueue_gmax(t, acc, GI);
-        if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) check_compact(flush_at, a.slack);
+        if (a.gmax != 2 && last_group && ((t + 1) % SR == 0 || t + 1 == ntiles))
+          check_compact(flush_at, a.slack);
         return;
       }
       DG_T0(t_h);
@@ -1357,6 +1381,11 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mh), __float_as_uint(mh),
                                                        false, false);
       const float m = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      if (a.gmax == 2) {  // dense tile maxima: one 128-B store, no test
+        if (h == 0) dense_tmax(u, t)[col] = m;
+        vmc += 1;
+        return;
+      }
       const uint64_t bal = __ballot(h == 0 && m > thr[u]);
       if (bal == 0ull || i_end - tile0 < kTileItems) return;  // a partial last tile is skipped
       DG_T0(t_e);
@@ -1388,6 +1417,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
       if constexpr (STAGED) {
         if (nblk > 0) resolve(IC<DR_RESOLVE_BATCHED>{});
       }
+      if (GMAX && a.gmax == 2) return;  // dense tile maxima: no buffers
       check_compact(flush_at, a.slack);
     };
     if constexpr (UTP) {

@@ -303,6 +303,83 @@ __global__ __launch_bounds__(256) void topk_threshold_kernel(
   if (thr2 && lane == (k - 1) / P) thr2[u] = below_key(dr::select_key<P>(key, (k - 1) % P));
 }
 
+// The same thresholds from the dense tile maxima of a gmax == 2 sample scan
+// (TopkArgs::tmax): one THREAD per user position of [0, n_pad) streams its
+// column ([user / 32][tile][user % 32]: a wave reads two 128-B lines per tile,
+// 8 tiles in flight) through a descending register array of its KS best
+// maxima. Insertion is a branch-free network, new[j] = max(old[j],
+// min(old[j-1], v)), 2 VALU per entry, run when some lane's maximum beats its
+// KS-th best. The k-th best tile maximum equals the k-th best key of the
+// compaction path's buffer (same maxima, same rank), so the thresholds are
+// bit-identical to it. NaN maxima (a tile whose 32 scores are all NaN) rank
+// nothing: a lower bound either way. KS >= k >= k1.
+constexpr int kDenseMaxKs = 32;
+constexpr size_t kDenseMaxBytes = (size_t)16 << 30;
+
+__device__ __forceinline__ float below_score(float s) {
+  const float b = s - fmaxf(fabsf(s) * 0x1p-20f, 0x1p-100f);
+  return b < s ? b : -INFINITY;  // -inf / +inf: no pruning
+}
+
+template <int KS>
+__global__ __launch_bounds__(256) void topk_threshold_dense_kernel(
+    const float* __restrict__ tmax, int64_t T, int64_t n_pad, int64_t n_users, int k, int k1,
+    float* __restrict__ thr, float* __restrict__ thr2) {
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (u >= n_pad) return;
+  if (u >= n_users) {
+    thr[u] = INFINITY;
+    if (thr2) thr2[u] = INFINITY;
+    return;
+  }
+  const float* src = tmax + (size_t)(u >> 5) * (size_t)T * 32 + (u & 31);
+  float best[KS];
+#pragma unroll
+  for (int j = 0; j < KS; ++j) best[j] = -INFINITY;
+  auto insert = [&](float v) {
+    v = v == v ? v : -INFINITY;
+    if (v > best[KS - 1]) {
+#pragma unroll
+      for (int j = KS - 1; j > 0; --j) best[j] = fmaxf(best[j], fminf(best[j - 1], v));
+      best[0] = fmaxf(best[0], v);
+    }
+  };
+  constexpr int kIn = 8;
+  int64_t t = 0;
+  for (; t + kIn <= T; t += kIn) {
+    float v[kIn];
+#pragma unroll
+    for (int i = 0; i < kIn; ++i) v[i] = src[(size_t)(t + i) * 32];
+#pragma unroll
+    for (int i = 0; i < kIn; ++i) insert(v[i]);
+  }
+  for (; t < T; ++t) insert(src[(size_t)t * 32]);
+  float v1 = -INFINITY, v2 = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < KS; ++j) {
+    if (j == k1 - 1) v1 = best[j];
+    if (j == k - 1) v2 = best[j];
+  }
+  thr[u] = below_score(v1);
+  if (thr2) thr2[u] = below_score(v2);
+}
+
+// Launch topk_threshold_dense_kernel for ranks (k1, k) over positions [0, n_pad).
+bool launch_threshold_dense(const float* tmax, int64_t T, int64_t n_pad, int64_t n_users, int k,
+                            int k1, float* thr, float* thr2, hipStream_t s) {
+  const dim3 grid((unsigned)dr::ceil_div(n_pad, 256));
+#define DR_TD(KK) \
+  hipLaunchKernelGGL((topk_threshold_dense_kernel<KK>), grid, dim3(256), 0, s, tmax, T, n_pad, \
+                     n_users, k, k1, thr, thr2)
+  if (k <= 8) DR_TD(8);
+  else if (k <= 16) DR_TD(16);
+  else if (k <= 24) DR_TD(24);
+  else if (k <= 32) DR_TD(32);
+  else return false;
+#undef DR_TD
+  return true;
+}
+
 // ------------------------------------------------------------------ merge
 // One wave per user: gather parts*k_in (score, item) pairs, sort, keep k_out.
 template <int P>
@@ -608,9 +685,24 @@ size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 //    fail thresholds | tier-2 fail rows | tier-2 fail positions | fail counts | diag].
 // The sample scan, the main scan and the rescans run one after the other on
 // the stream and share the candidate region.
+// The sample scan keeps dense tile maxima (TopkArgs::gmax == 2) when its rank
+// fits the dense threshold kernel and the [users][tiles] float matrix fits
+// kDenseMaxBytes (it shares the candidate region: the main scan starts after
+// the thresholds are read); else the compaction path (gmax == 1).
+// DR_KNOB_SAMPLE_DENSE = 0 forces the compaction path (A/B and the
+// bit-identity test of the two).
+bool sample_dense(int ks, int64_t n_users_pad, int64_t S) {
+  if (knob_int(DR_KNOB_SAMPLE_DENSE, 1) == 0) return false;
+  return ks <= kDenseMaxKs && (size_t)n_users_pad * (size_t)(S / kTileItems) * 4 <= kDenseMaxBytes;
+}
+size_t dense_bytes(int64_t n_users_pad, int64_t S) {
+  return (size_t)n_users_pad * (size_t)(S / kTileItems) * 4;
+}
+
 struct Layout {
   Plan main, sample;
   Guess g;
+  bool dense = false;  // the sample scan keeps dense tile maxima
   size_t cand = 0, cnt = 0, thr = 0, samp = 0, frows = 0, fpos = 0, fthr = 0, fcnt = 0, diag = 0;
   size_t off_thr() const { return cand + cnt; }
   size_t off_samp() const { return off_thr() + 2 * thr; }
@@ -635,7 +727,9 @@ Layout make_layout(int64_t n_users, int64_t n_items, int w, int k) {
     // the sample keeps only ks keys per user: compact it tighter
     L.sample.slack = kSampleSlack;
     L.sample.gap = kSampleGap;
-    L.cand = L.cand > L.sample.cand_bytes ? L.cand : L.sample.cand_bytes;
+    L.dense = sample_dense(L.g.ks, L.sample.n_users_pad, L.g.S);
+    const size_t sb = L.dense ? al256(dense_bytes(L.sample.n_users_pad, L.g.S)) : L.sample.cand_bytes;
+    L.cand = L.cand > sb ? L.cand : sb;
     L.cnt = L.cnt > L.sample.cnt_bytes ? L.cnt : L.sample.cnt_bytes;
     L.thr = al256((size_t)L.main.n_users_pad * sizeof(float));
     L.samp = al256((size_t)L.g.S * w * 2);
@@ -936,10 +1030,19 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   as.head_keep = ps.head_keep;
   as.slack = ps.slack;
   as.gap = ps.gap;
-  as.gmax = DR_SAMPLE_GMAX;
+  as.gmax = L.dense ? 2 : DR_SAMPLE_GMAX;
+  as.tmax = (float*)ws;  // the candidate region
+  as.tmax_tiles = L.g.S / kTileItems;
   DR_SCAN_OR_FAIL(ps, as, false)
   DR_CHECK_LAUNCH();
-  {
+  if (L.dense) {
+    if (!launch_threshold_dense(as.tmax, as.tmax_tiles, p.n_users_pad, n_users, L.g.ks, L.g.ks1,
+                                thr, thr2, s)) {
+      dr::set_error("dr_score_topk: internal plan error (dense threshold rank)");
+      return DR_EUNSUPPORTED;
+    }
+    DR_CHECK_LAUNCH();
+  } else {
     const BufMap sm = buf_map(ps);
     const int64_t sh = ps.head_users();
 #define DR_THR(PP)                                                                             \
@@ -1157,6 +1260,7 @@ extern "C" int dr_score_topk_seeded(const void* user_table, const int64_t* user_
 struct SampleThrLayout {
   Plan p;
   int64_t S = 0;
+  bool dense = false;
   size_t cand = 0, cnt = 0, samp = 0;
   size_t total() const { return cand + cnt + samp; }
 };
@@ -1168,7 +1272,8 @@ SampleThrLayout sample_thr_layout(int64_t n_users, int64_t n_sample, int w, int 
   L.p = make_plan(n_users, L.S, w, ks, false);
   L.p.slack = kSampleSlack;
   L.p.gap = kSampleGap;
-  L.cand = al256(L.p.cand_bytes);
+  L.dense = sample_dense(ks, L.p.n_users_pad, L.S);
+  L.cand = al256(L.dense ? dense_bytes(L.p.n_users_pad, L.S) : L.p.cand_bytes);
   L.cnt = al256(L.p.cnt_bytes);
   L.samp = al256((size_t)L.S * w * 2);
   return L;
@@ -1252,7 +1357,9 @@ extern "C" int dr_sample_thresholds(const void* user_table, const int64_t* user_
   a.head_keep = p.head_keep;
   a.slack = p.slack;
   a.gap = p.gap;
-  a.gmax = 1;
+  a.gmax = L.dense ? 2 : 1;
+  a.tmax = (float*)ws;
+  a.tmax_tiles = L.S / kTileItems;
   a.cand = (uint64_t*)ws;
   a.cnt = (int32_t*)(ws + L.cand);
   if (!launch_scan(p, a, dtype, w, false, s)) {
@@ -1260,6 +1367,14 @@ extern "C" int dr_sample_thresholds(const void* user_table, const int64_t* user_
     return DR_EUNSUPPORTED;
   }
   DR_CHECK_LAUNCH();
+  if (L.dense) {
+    if (!launch_threshold_dense(a.tmax, a.tmax_tiles, n_users, n_users, ks, ks1, thr1, thr2, s)) {
+      dr::set_error("dr_sample_thresholds: internal plan error (dense threshold rank)");
+      return DR_EUNSUPPORTED;
+    }
+    DR_CHECK_LAUNCH();
+    return DR_OK;
+  }
   const BufMap sm = buf_map(p);
   const int64_t sh = p.head_users() < n_users ? p.head_users() : n_users;
   int64_t T0 = 0, T1 = sh;

@@ -10,7 +10,7 @@ import pytest
 import torch
 
 import oracle
-from divrec import ops
+from divrec import _backend, ops
 from topk_checks import fp32_row_tol, gap_check
 
 pytestmark = pytest.mark.gpu
@@ -1035,16 +1035,20 @@ def test_padded_item_table_sees_data_writes():
     assert not torch.equal(p1, p2)
 
 
+@pytest.mark.parametrize("dense", [1, 0])
 @pytest.mark.parametrize("d,n_sample,ks1,ks,ids", [(128, 78125, 5, 10, False), (64, 31250, 10, 17, True),
                                                    (128, 70, 1, 3, False), (64, 5000, 50, 68, True),
-                                                   (32, 31, 1, 2, False)])
-def test_sample_thresholds_group_max(d, n_sample, ks1, ks, ids):
+                                                   (32, 31, 1, 2, False), (64, 40000, 29, 32, False)])
+def test_sample_thresholds_group_max(d, n_sample, ks1, ks, ids, dense):
     """dr_sample_thresholds (the item-sharded path's guess): the whole 32-row
     tiles of the sample, tile-transposed (sample q T + r -> row q of tile r),
     one max per user and tile (its 32 rows), thresholds strictly below each
     user's ks1-th / ks-th best tile max (-inf with fewer tiles). Integer tables:
     every score exact, so the thresholds must equal a torch restatement bit for
-    bit, and never exceed the exact sample ranks."""
+    bit, and never exceed the exact sample ranks. Both forms of the sample
+    scan: dense tile maxima ranked per user by topk_threshold_dense_kernel
+    (ks <= 32, the default) and the compaction path (sample_dense = 0, and
+    ks = 68 with the default)."""
     from divrec.distributed import threshold_below
 
     rng = np.random.default_rng(d + n_sample + ks)
@@ -1053,8 +1057,9 @@ def test_sample_thresholds_group_max(d, n_sample, ks1, ks, ids):
     Sm = _int_table(rng, n_sample, d)
     uids = rng.permutation(nu)[:1800].astype(np.int64) if ids else None
     Ub, Sb = _bf16(U), _bf16(Sm)
-    out = ops.sample_thresholds(Ub, Sb, ks1, ks,
-                                user_ids=None if uids is None else torch.from_numpy(uids).to(DEV))
+    with _backend.plan_knobs(sample_dense=dense):
+        out = ops.sample_thresholds(Ub, Sb, ks1, ks,
+                                    user_ids=None if uids is None else torch.from_numpy(uids).to(DEV))
     Uq = U if uids is None else U[uids]
     Sp = n_sample // 32 * 32
     ref = torch.full((2, Uq.shape[0]), -float("inf"))
@@ -1071,6 +1076,36 @@ def test_sample_thresholds_group_max(d, n_sample, ks1, ks, ids):
                            descending=True).values
         assert (ref[1].double() <= exact[:, ks - 1]).all()  # a lower bound of the exact rank
     assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("d,k,dtype", [(64, 100, torch.bfloat16), (128, 100, torch.bfloat16),
+                                       (32, 20, torch.bfloat16), (64, 100, torch.float32)])
+def test_score_topk_dense_sample_matches_compaction(d, k, dtype):
+    """The guessed-threshold path with the sample scan's dense tile maxima
+    (round 5, the default for ks <= 32) against its compaction path
+    (sample_dense = 0): the thresholds are the same order statistic of the same
+    tile maxima, so the first-tier / second-tier failure counts must be equal
+    and the lists identical, and identical to the unseeded scan's.
+    Random-normal tables (realistic, tie-free thresholds); 4100 users: several
+    user blocks, the last one partial; 300K rows: seeded at stride 32."""
+    rng = np.random.default_rng(d * 3 + k)
+    nu, ni = 4100, 300_011
+    U = (rng.standard_normal((nu, d)) / np.sqrt(d)).astype(np.float32)
+    I = (rng.standard_normal((ni, d)) / np.sqrt(d)).astype(np.float32)
+    Ut, It = torch.from_numpy(U).to(DEV).to(dtype), torch.from_numpy(I).to(DEV).to(dtype)
+    plan = ops.score_topk_plan(nu, ni, dtype, d, k)
+    assert plan["sample_stride"] == 32 and plan["sample_rank"] <= 32
+    out = {}
+    for dense in (1, 0):
+        st = {}
+        with _backend.plan_knobs(sample_dense=dense):
+            s, i = ops.score_topk(Ut, It, k, stats=st)
+        out[dense] = (s.cpu(), i.cpu(), st["guess_failures"])
+    assert out[1][2] == out[0][2]
+    assert torch.equal(out[1][1], out[0][1]) and torch.equal(out[1][0], out[0][0])
+    with _backend.plan_knobs(scan_seed=0):  # the plain scan from -inf: same scores, same order
+        s0, i0 = ops.score_topk(Ut, It, k)
+    assert torch.equal(out[1][1], i0.cpu()) and torch.equal(out[1][0], s0.cpu())
 
 
 @pytest.mark.parametrize("d,k", [(128, 129), (64, 300), (256, 200), (32, 1000), (128, 1000)])

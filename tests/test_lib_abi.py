@@ -135,12 +135,18 @@ def test_workspace_reflects_split_tail_plan():
     whole and each of the 209 tail blocks is split into 6 chunks, whose extra
     candidate buffers (5 x 209 x 1024 rows of CAP 512 keys) the workspace
     holds; with the split off (scan_split = 1) only one buffer per user
-    remains (DESIGN.md §3.1 grid tail)."""
+    remains (DESIGN.md §3.1 grid tail). The seeded plan's sample scan keeps
+    dense tile maxima in the same region: 2441 tiles of the 78K-row sample x
+    the padded users x 4 B, larger than the buffers here (sample_dense = 0:
+    the compaction path, buffers only)."""
     lib = _backend.load_library()
     bf16 = _backend.DR_BF16
     one = (1_000_000 + 448) * 512 * 8  # padded users x CAP x 8 B
     extra = 5 * 209 * 1024 * 512 * 8
+    dense = (1_000_000 + 448) * (10_000_000 // 128 // 32) * 4
     with _backend.plan_knobs(scan_slots=256):
+        assert dense <= lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100) < dense + 200_000_000
+    with _backend.plan_knobs(scan_slots=256, sample_dense=0):
         split = lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100)
         assert one + extra <= split < one + extra + 200_000_000
         with _backend.plan_knobs(scan_split=1):
@@ -158,8 +164,8 @@ def test_plan_knobs_set_restore_and_no_environment(monkeypatch):
     import math
     lib = _backend.load_library()
     bf16 = _backend.DR_BF16
-    assert all(math.isnan(lib.dr_get_plan_knob(i)) for i in range(8))
-    assert lib.dr_set_plan_knob(8, 1.0) == -1  # DR_EINVAL: unknown knob
+    assert all(math.isnan(lib.dr_get_plan_knob(i)) for i in range(9))
+    assert lib.dr_set_plan_knob(9, 1.0) == -1  # DR_EINVAL: unknown knob
     out = (ctypes.c_int64 * 13)()
     assert lib.dr_score_topk_plan(1_000_000, 10_000_000, bf16, 128, 100, out, 13) == 0
     base = list(out)
