@@ -306,15 +306,22 @@ __global__ __launch_bounds__(256) void topk_threshold_kernel(
 // The same thresholds from the dense tile maxima of a gmax == 2 sample scan
 // (TopkArgs::tmax): one THREAD per user position of [0, n_pad) streams its
 // column ([user / 32][tile][user % 32]: a wave reads two 128-B lines per tile,
-// 8 tiles in flight) through a descending register array of its KS best
-// maxima. Insertion is a branch-free network, new[j] = max(old[j],
-// min(old[j-1], v)), 2 VALU per entry, run when some lane's maximum beats its
-// KS-th best. The k-th best tile maximum equals the k-th best key of the
-// compaction path's buffer (same maxima, same rank), so the thresholds are
-// bit-identical to it. NaN maxima (a tile whose 32 scores are all NaN) rank
-// nothing: a lower bound either way. KS >= k >= k1.
-constexpr int kDenseMaxKs = 32;
-constexpr size_t kDenseMaxBytes = (size_t)16 << 30;
+// 8 tiles in flight) into a descending register array of its KS best maxima.
+// A maximum above the lane's cut (its KS-th best at the last merge) is
+// appended to the lane's LDS list (kDenseBuf slots); when some lane's list
+// could overflow, every lane merges its list through a branch-free insertion
+// network, new[j] = max(old[j], min(old[j-1], v)) (2 VALU per entry), and
+// raises its cut. Appends cost ~3 VALU per tile; merges run ~KS (1 + ln(T /
+// KS)) / kDenseBuf times per wave instead of once per tile (the wave's lanes
+// insert at different tiles: a per-tile network ran on nearly every tile).
+// Values at or below the cut cannot change the KS-th order statistic. The
+// k-th best tile maximum equals the k-th best key of the compaction path's
+// buffer (same maxima, same rank), so the thresholds are bit-identical to it.
+// NaN maxima (a tile whose 32 scores are all NaN) rank nothing: a lower bound
+// either way. KS >= k >= k1.
+constexpr int kDenseMaxKs = 72;
+constexpr int kDenseBuf = 24;
+constexpr double kDenseMaxGiB = 16.0;
 
 __device__ __forceinline__ float below_score(float s) {
   const float b = s - fmaxf(fabsf(s) * 0x1p-20f, 0x1p-100f);
@@ -325,35 +332,56 @@ template <int KS>
 __global__ __launch_bounds__(256) void topk_threshold_dense_kernel(
     const float* __restrict__ tmax, int64_t T, int64_t n_pad, int64_t n_users, int k, int k1,
     float* __restrict__ thr, float* __restrict__ thr2) {
+  constexpr int kIn = 8;
+  static_assert(kDenseBuf >= kIn, "a merge leaves room for one batch");
+  __shared__ float lst[4][kDenseBuf][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (u >= n_pad) return;
-  if (u >= n_users) {
-    thr[u] = INFINITY;
-    if (thr2) thr2[u] = INFINITY;
-    return;
-  }
-  const float* src = tmax + (size_t)(u >> 5) * (size_t)T * 32 + (u & 31);
+  if (__builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * 256 + (threadIdx.x & ~63)) >= n_pad)))
+    return;  // whole wave past the end
+  const bool live = u < n_users;
+  const float* src = tmax + (size_t)((live ? u : 0) >> 5) * (size_t)T * 32 + (u & 31);
   float best[KS];
 #pragma unroll
   for (int j = 0; j < KS; ++j) best[j] = -INFINITY;
-  auto insert = [&](float v) {
-    v = v == v ? v : -INFINITY;
-    if (v > best[KS - 1]) {
+  float cut = -INFINITY;
+  int n = 0;
+  auto merge = [&]() {
+    for (int i = 0; __builtin_amdgcn_ballot_w64(i < n) != 0ull; ++i) {
+      const float v = i < n ? lst[wave][i][lane] : -INFINITY;
 #pragma unroll
       for (int j = KS - 1; j > 0; --j) best[j] = fmaxf(best[j], fminf(best[j - 1], v));
       best[0] = fmaxf(best[0], v);
     }
+    n = 0;
+    cut = best[KS - 1];
   };
-  constexpr int kIn = 8;
+  auto add = [&](float v) {
+    v = v == v ? v : -INFINITY;
+    if (v > cut) lst[wave][n++][lane] = v;
+  };
   int64_t t = 0;
-  for (; t + kIn <= T; t += kIn) {
-    float v[kIn];
+  if (live) {
+    for (; t + kIn <= T; t += kIn) {
+      float v[kIn];
 #pragma unroll
-    for (int i = 0; i < kIn; ++i) v[i] = src[(size_t)(t + i) * 32];
+      for (int i = 0; i < kIn; ++i) v[i] = src[(size_t)(t + i) * 32];
 #pragma unroll
-    for (int i = 0; i < kIn; ++i) insert(v[i]);
+      for (int i = 0; i < kIn; ++i) add(v[i]);
+      if (__builtin_amdgcn_ballot_w64(n > kDenseBuf - kIn) != 0ull) merge();
+    }
+    for (; t < T; ++t) {
+      add(src[(size_t)t * 32]);
+      if (__builtin_amdgcn_ballot_w64(n >= kDenseBuf) != 0ull) merge();
+    }
   }
-  for (; t < T; ++t) insert(src[(size_t)t * 32]);
+  merge();
+  if (u >= n_pad) return;
+  if (!live) {
+    thr[u] = INFINITY;
+    if (thr2) thr2[u] = INFINITY;
+    return;
+  }
   float v1 = -INFINITY, v2 = -INFINITY;
 #pragma unroll
   for (int j = 0; j < KS; ++j) {
@@ -375,6 +403,8 @@ bool launch_threshold_dense(const float* tmax, int64_t T, int64_t n_pad, int64_t
   else if (k <= 16) DR_TD(16);
   else if (k <= 24) DR_TD(24);
   else if (k <= 32) DR_TD(32);
+  else if (k <= 48) DR_TD(48);
+  else if (k <= 72) DR_TD(72);
   else return false;
 #undef DR_TD
   return true;
@@ -687,13 +717,15 @@ size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 // the stream and share the candidate region.
 // The sample scan keeps dense tile maxima (TopkArgs::gmax == 2) when its rank
 // fits the dense threshold kernel and the [users][tiles] float matrix fits
-// kDenseMaxBytes (it shares the candidate region: the main scan starts after
+// kDenseMaxGiB (it shares the candidate region: the main scan starts after
 // the thresholds are read); else the compaction path (gmax == 1).
 // DR_KNOB_SAMPLE_DENSE = 0 forces the compaction path (A/B and the
-// bit-identity test of the two).
+// bit-identity test of the two); a value > 1 is the budget in GiB.
 bool sample_dense(int ks, int64_t n_users_pad, int64_t S) {
-  if (knob_int(DR_KNOB_SAMPLE_DENSE, 1) == 0) return false;
-  return ks <= kDenseMaxKs && (size_t)n_users_pad * (size_t)(S / kTileItems) * 4 <= kDenseMaxBytes;
+  double gib = kDenseMaxGiB;
+  if (dr::plan_knob(DR_KNOB_SAMPLE_DENSE, &gib) && gib <= 0.0) return false;
+  if (gib <= 1.0) gib = kDenseMaxGiB;  // 1: on, default budget
+  return ks <= kDenseMaxKs && (double)n_users_pad * (double)(S / kTileItems) * 4.0 <= gib * 1073741824.0;
 }
 size_t dense_bytes(int64_t n_users_pad, int64_t S) {
   return (size_t)n_users_pad * (size_t)(S / kTileItems) * 4;

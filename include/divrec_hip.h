@@ -65,7 +65,7 @@ enum dr_plan_knob {
   DR_KNOB_GUESS_Z1 = 5,     /* first-tier margin z (ks1 = mu + z sigma + c1) */
   DR_KNOB_GUESS_C1 = 6,     /* first-tier offset c1 */
   DR_KNOB_GUESS_TIGHT = 7,  /* 0: one tier (ks1 = ks) */
-  DR_KNOB_SAMPLE_DENSE = 8, /* 0: the sample scan compacts key buffers instead of dense tile maxima */
+  DR_KNOB_SAMPLE_DENSE = 8, /* 0: sample scan on compacted key buffers, not dense tile maxima; >1: budget GiB */
   DR_KNOB_COUNT = 9
 };
 /* Set knob `knob` to `value` (NaN = default). DR_EINVAL for an unknown knob. */

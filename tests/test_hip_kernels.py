@@ -1079,10 +1079,11 @@ def test_sample_thresholds_group_max(d, n_sample, ks1, ks, ids, dense):
 
 
 @pytest.mark.parametrize("d,k,dtype", [(64, 100, torch.bfloat16), (128, 100, torch.bfloat16),
-                                       (32, 20, torch.bfloat16), (64, 100, torch.float32)])
+                                       (32, 20, torch.bfloat16), (64, 100, torch.float32),
+                                       (128, 1000, torch.bfloat16)])
 def test_score_topk_dense_sample_matches_compaction(d, k, dtype):
     """The guessed-threshold path with the sample scan's dense tile maxima
-    (round 5, the default for ks <= 32) against its compaction path
+    (round 5, the default for ks <= 72; k = 1000: ks = 68) against its compaction path
     (sample_dense = 0): the thresholds are the same order statistic of the same
     tile maxima, so the first-tier / second-tier failure counts must be equal
     and the lists identical, and identical to the unseeded scan's.
@@ -1094,7 +1095,7 @@ def test_score_topk_dense_sample_matches_compaction(d, k, dtype):
     I = (rng.standard_normal((ni, d)) / np.sqrt(d)).astype(np.float32)
     Ut, It = torch.from_numpy(U).to(DEV).to(dtype), torch.from_numpy(I).to(DEV).to(dtype)
     plan = ops.score_topk_plan(nu, ni, dtype, d, k)
-    assert plan["sample_stride"] == 32 and plan["sample_rank"] <= 32
+    assert plan["sample_stride"] == 32 and plan["sample_rank"] <= 72
     out = {}
     for dense in (1, 0):
         st = {}
