@@ -68,7 +68,7 @@ enum {
 #define DR_RING 3  // ring slots (RING - 1 stages in flight), d != 128
 #endif
 #ifndef DR_STAGE_BYTES_WIDE
-#define DR_STAGE_BYTES_WIDE 65536  // ring slot for d = 128
+#define DR_STAGE_BYTES_WIDE 73728  // ring slot for d = 128 (9 tiles: 72 KB; 64 KB measured +0.4-0.8 %)
 #endif
 #ifndef DR_RING_WIDE
 #define DR_RING_WIDE 2  // ring slots for d = 128
@@ -131,10 +131,11 @@ constexpr int kTileItems = 32;
 constexpr int kSlack = DR_SLACK;  // keys kept beyond k by a compaction
 constexpr int kFlushGap = DR_FLUSH_GAP;
 
-// Stage geometry per row width. d = 128: two 64-KB slots (one barrier per
-// 8 tiles at d=128; measured against three 32-KB slots: +2 % at 10M items,
-// +6 % at 1.25M, where the survivor stream makes per-stage wave imbalance
-// larger). d <= 64: three 32-KB slots (its LDS survivor staging needs room;
+// Stage geometry per row width. d = 128: two 72-KB slots (one barrier per
+// 9 tiles; measured against three 32-KB slots: +2 % at 10M items, +6 % at
+// 1.25M, where the survivor stream makes per-stage wave imbalance larger;
+// round 5: against two 64-KB slots -0.4 to -0.8 % at 10M, -0.35 to -0.65 % at
+// k = 1000, +0.1 % at 1.25M; three 48-KB slots +1 to +2.6 %). d <= 64: three 32-KB slots (its LDS survivor staging needs room;
 // 64-KB stages measured -10 % there; d = 256 spills with them).
 #ifndef DR_STAGE_BYTES_NARROW
 #define DR_STAGE_BYTES_NARROW DR_STAGE_BYTES  // ring slot for d <= 64
@@ -142,7 +143,10 @@ constexpr int kFlushGap = DR_FLUSH_GAP;
 constexpr int stage_bytes_for(int w) {
   return w == 128 ? DR_STAGE_BYTES_WIDE : (w <= 64 ? DR_STAGE_BYTES_NARROW : DR_STAGE_BYTES);
 }
-constexpr int ring_for(int w) { return w == 128 ? DR_RING_WIDE : DR_RING; }
+#ifndef DR_RING_NARROW
+#define DR_RING_NARROW DR_RING  // ring slots for d <= 64
+#endif
+constexpr int ring_for(int w) { return w == 128 ? DR_RING_WIDE : (w <= 64 ? DR_RING_NARROW : DR_RING); }
 
 template <int D>  // D = W, the row's width in bf16 units (row bytes / 2)
 struct TileGeom {

@@ -1109,6 +1109,31 @@ def test_score_topk_dense_sample_matches_compaction(d, k, dtype):
     assert torch.equal(out[1][1], i0.cpu()) and torch.equal(out[1][0], s0.cpu())
 
 
+@pytest.mark.parametrize("slots", [0, 7])
+def test_score_topk_dense_sample_chunked_units(slots):
+    """Few users over a long catalog: one user block, so the sample plan splits
+    its 131072 sample rows into catalog chunks (two on 256 slots; more with 7
+    planned slots), each unit writing its tiles' maxima at the global tile
+    index. Dense and compaction sample scans and the unseeded scan give
+    identical lists, and the lists are exact (integer tables)."""
+    rng = np.random.default_rng(4242 + slots)
+    nu, ni, d, k = 70, 32 * 131072 + 45, 32, 300
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    Ut, It = _bf16(U), _bf16(I)
+    plan = ops.score_topk_plan(nu, ni, torch.bfloat16, d, k)
+    assert plan["sample_stride"] == 32 and plan["sample_rows"] == 131072
+    knobs = {"scan_slots": slots} if slots else {}
+    out = []
+    for extra in ({}, {"sample_dense": 0}, {"scan_seed": 0}):
+        with _backend.plan_knobs(**knobs, **extra):
+            s, i = ops.score_topk(Ut, It, k)
+        out.append((s.cpu(), i.cpu()))
+    for s, i in out[1:]:
+        assert torch.equal(i, out[0][1]) and torch.equal(s, out[0][0])
+    ref_i, ref_s = _exact_topk_torch(U, I, k)
+    assert np.array_equal(out[0][1].numpy().astype(np.int64), ref_i)
+
+
 @pytest.mark.parametrize("d,k", [(128, 129), (64, 300), (256, 200), (32, 1000), (128, 1000)])
 @pytest.mark.parametrize("kind", ["cosine", "dot", "euclidean"])
 def test_ild_embedding_long_lists(d, k, kind):
