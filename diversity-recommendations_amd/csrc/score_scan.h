@@ -135,16 +135,19 @@ constexpr int kFlushGap = DR_FLUSH_GAP;
 // 9 tiles; measured against three 32-KB slots: +2 % at 10M items, +6 % at
 // 1.25M, where the survivor stream makes per-stage wave imbalance larger;
 // round 5: against two 64-KB slots -0.4 to -0.8 % at 10M, -0.35 to -0.65 % at
-// k = 1000, +0.1 % at 1.25M; three 48-KB slots +1 to +2.6 %). d <= 64: three 32-KB slots (its LDS survivor staging needs room;
-// 64-KB stages measured -10 % there; d = 256 spills with them).
+// k = 1000, +0.1 % at 1.25M; three 48-KB slots +1 to +2.6 %). d <= 64 (its
+// LDS survivor staging needs room): two 48-KB slots, a barrier every 12 tiles
+// at d = 64 (round 5, against three 32-KB slots: -0.4 to -0.9 % at config 2,
+// -1.6 % at d = 32; four 24-KB slots +3.5 %; the stage margin of 384 keys puts
+// k = 100 on CAP 1024 there). d = 256 spills with 64-KB stages.
 #ifndef DR_STAGE_BYTES_NARROW
-#define DR_STAGE_BYTES_NARROW DR_STAGE_BYTES  // ring slot for d <= 64
+#define DR_STAGE_BYTES_NARROW 49152  // ring slot for d <= 64
 #endif
 constexpr int stage_bytes_for(int w) {
   return w == 128 ? DR_STAGE_BYTES_WIDE : (w <= 64 ? DR_STAGE_BYTES_NARROW : DR_STAGE_BYTES);
 }
 #ifndef DR_RING_NARROW
-#define DR_RING_NARROW DR_RING  // ring slots for d <= 64
+#define DR_RING_NARROW 2  // ring slots for d <= 64
 #endif
 constexpr int ring_for(int w) { return w == 128 ? DR_RING_WIDE : (w <= 64 ? DR_RING_NARROW : DR_RING); }
 
