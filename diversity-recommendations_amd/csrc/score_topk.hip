@@ -18,6 +18,7 @@
 // result is a deterministic total order and any item partition (chunks,
 // GPUs) gives bit-identical top-k lists.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 #include "score_scan.h"
@@ -644,12 +645,27 @@ struct Guess {
 #define DR_GUESS_STRIDE 32
 #endif
 // Two-tier guess (round 3): the main scan starts from the sample's
-// ks1-th best score, ks1 = mean + DR_GUESS_TIGHT_Z sigma + 1 (about 0.1 %
-// of users fail it); the users it fails are rescanned from their safe
+// ks1-th best score; the users it fails are rescanned from their safe
 // (6-sigma) threshold by a second-tier scan spread over every CU, and the
 // rare users that fail that too by the whole-catalog rescan from -inf.
-#ifndef DR_GUESS_TIGHT_Z
-#define DR_GUESS_TIGHT_Z 3.0
+// ks1 (round 5) is the smallest rank whose Poisson(mu) tail P(X >= ks1) is at
+// most DR_GUESS_TAIL = 0.5 % (the share of users expected to fail it); the
+// round-3 rule mu + 3 sigma + 1 had tails of 0.12-0.15 %. Measured with the
+// z knob giving the same ranks (profiles/r05/ab19/, ab20/, lists identical):
+// config 2 (ks1 10 -> 9) -1.05 %, d = 32 -2.7 %, an 8-way shard's 1.25M rows
+// -0.8 %, k = 1000 (50 -> 48) -0.2 %; the headline keeps 5 (the 0.84 % tail
+// of 4 measured +0.1 %).
+int poisson_tail_rank(double mu, double tail) {
+  double pmf = std::exp(-mu), cdf = 0.0;
+  for (int j = 1; j < 4096; ++j) {
+    cdf += pmf;                         // P(X <= j - 1)
+    if (1.0 - cdf <= tail) return j;    // P(X >= j)
+    pmf *= mu / (double)j;
+  }
+  return 4096;
+}
+#ifndef DR_GUESS_TAIL
+#define DR_GUESS_TAIL 0.005
 #endif
 constexpr int kMaxRescanChunks = 64;  // catalog chunks per user block of a second-tier rescan
 constexpr int64_t kGuessStride = DR_GUESS_STRIDE;
@@ -690,10 +706,11 @@ Guess guess_for(int64_t n_items, int k, bool split_tail) {
   const double mu = (double)k * (double)g.S / (double)n_items;
   int ks = (int)ceil(mu + DR_GUESS_SIGMA * sqrt(mu) + 3.0);
   g.ks = ks < k ? ks : k;
-  double z1 = DR_GUESS_TIGHT_Z, c1 = 1.0;
-  dr::plan_knob(DR_KNOB_GUESS_Z1, &z1);  // A/B knobs
-  dr::plan_knob(DR_KNOB_GUESS_C1, &c1);
-  int ks1 = (int)ceil(mu + z1 * sqrt(mu) + c1);
+  int ks1 = poisson_tail_rank(mu, DR_GUESS_TAIL);
+  double z1 = 3.0, c1 = 1.0;
+  const bool zk = dr::plan_knob(DR_KNOB_GUESS_Z1, &z1);  // A/B knobs: the round-3 form
+  const bool ck = dr::plan_knob(DR_KNOB_GUESS_C1, &c1);
+  if (zk || ck) ks1 = (int)ceil(mu + z1 * sqrt(mu) + c1);
   if (ks1 < 1) ks1 = 1;
   if (knob_int(DR_KNOB_GUESS_TIGHT, 1) == 0) ks1 = g.ks;  // A/B knob: one tier (ks1 = ks)
   g.ks1 = ks1 < g.ks ? ks1 : g.ks;

@@ -184,7 +184,7 @@ def global_mean(values: torch.Tensor, group=None) -> torch.Tensor:
 # Every tier is verified after the merge (a user with fewer than k merged items
 # failed it), so the result is the exact global top-k in every case.
 GUESS_SIGMA = 6.0
-GUESS_TIGHT_Z = 3.0
+GUESS_TAIL = 0.005  # first-tier rank: Poisson tail at most 0.5 % (csrc/score_topk.hip)
 # Observability of the last thresholded_exchange call, summed over the ranks
 # of its group (tests and the bench; not used by the path itself):
 # LAST_FALLBACK_USERS = users whose first-tier guess failed (recomputed by a
@@ -207,13 +207,24 @@ def guess_rank(k: int, frac: float) -> int:
     return min(k, int(math.ceil(mu + GUESS_SIGMA * math.sqrt(mu) + 3.0)))
 
 
+def poisson_tail_rank(mu: float, tail: float = GUESS_TAIL) -> int:
+    """Smallest j >= 1 with P(Poisson(mu) >= j) <= tail (score_topk.hip
+    poisson_tail_rank: the same double-precision recurrence)."""
+    pmf, cdf = math.exp(-mu), 0.0
+    for j in range(1, 4096):
+        cdf += pmf
+        if 1.0 - cdf <= tail:
+            return j
+        pmf *= mu / j
+    return 4096
+
+
 def guess_ranks(k: int, frac: float) -> Tuple[int, int]:
-    """(ks1, ks): the first-tier rank mu + 3 sigma + 1 (at most ks) and the safe
-    rank, as guess_for computes them."""
+    """(ks1, ks): the first-tier rank (the 0.5 % Poisson-tail rank of
+    mu = k * frac, at most ks) and the safe rank, as guess_for computes them."""
     mu = k * frac
     ks = guess_rank(k, frac)
-    ks1 = max(1, int(math.ceil(mu + GUESS_TIGHT_Z * math.sqrt(mu) + 1.0)))
-    return min(ks1, ks), ks
+    return min(max(1, poisson_tail_rank(mu)), ks), ks
 
 
 def threshold_below(kth: torch.Tensor) -> torch.Tensor:

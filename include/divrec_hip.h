@@ -62,8 +62,8 @@ enum dr_plan_knob {
   DR_KNOB_TAIL_KEYS = 2,    /* finalize key cap of a split-tail user */
   DR_KNOB_SCAN_SEED = 3,    /* 0: never seed from a sample; 1: always (>= 2^18 rows) */
   DR_KNOB_GUESS_STRIDE = 4, /* sample stride of the guessed thresholds */
-  DR_KNOB_GUESS_Z1 = 5,     /* first-tier margin z (ks1 = mu + z sigma + c1) */
-  DR_KNOB_GUESS_C1 = 6,     /* first-tier offset c1 */
+  DR_KNOB_GUESS_Z1 = 5,     /* set: ks1 = mu + z sigma + c1 instead of the 0.5 % Poisson-tail rank */
+  DR_KNOB_GUESS_C1 = 6,     /* set: the offset c1 of that form (z defaults to 3) */
   DR_KNOB_GUESS_TIGHT = 7,  /* 0: one tier (ks1 = ks) */
   DR_KNOB_SAMPLE_DENSE = 8, /* 0: sample scan on compacted key buffers, not dense tile maxima; >1: budget GiB */
   DR_KNOB_COUNT = 9

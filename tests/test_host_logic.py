@@ -230,10 +230,17 @@ def test_global_threshold_helpers():
     assert guess_rank(5, 0.9) == 5  # never above k
     from divrec.distributed import guess_ranks
 
-    assert guess_ranks(100, 1 / 32) == (10, 17)  # config 2: first tier 10, safe 17
+    # first tier: the smallest rank whose Poisson(mu) tail is <= 0.5 %
+    assert guess_ranks(100, 1 / 32) == (9, 17)  # config 2: first tier 9, safe 17
     assert guess_ranks(100, 78125 / 10_000_000) == (5, 10)
-    assert guess_ranks(1000, 1 / 32) == (50, 68)  # config 5's top-1000 scan
+    assert guess_ranks(1000, 1 / 32) == (48, 68)  # config 5's top-1000 scan
     assert guess_ranks(3, 0.01) == (2, 3)
+    from scipy.stats import poisson
+
+    from divrec.distributed import poisson_tail_rank
+    for mu in (0.03, 0.78, 1.5623, 3.125, 31.25, 200.0):
+        j = poisson_tail_rank(mu)
+        assert poisson.sf(j - 1, mu) <= 0.005 < (poisson.sf(j - 2, mu) if j > 1 else 1.0), mu
     s = torch.tensor([1.0, -2.5, 0.0, float("-inf"), float("nan"), 3e-39])
     t = threshold_below(s)
     assert bool((t[:3] < s[:3]).all()) and bool((t[5:] < s[5:]).all())

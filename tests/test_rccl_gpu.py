@@ -33,7 +33,7 @@ from divrec import ops
 pytestmark = pytest.mark.gpu
 
 NU, NI, D, K = 3 * 1024 + 77, 300_011, 64, 100
-N_TIER2, N_INF = 12, 40  # hot rows seen by each planted group (ks1 = 10 <= 12 < ks = 17 < 40)
+N_TIER2, N_INF = 12, 40  # hot rows seen by each planted group (ks1 = 9 <= 12 < ks = 17 < 40)
 
 
 def _free_port():

@@ -334,7 +334,7 @@ def test_config5_plan_1m_x_10m_k1000_then_mmr():
     two-tier guess, CAP 2048, long-list flush) and the MMR re-rank of those
     1000 candidates to 100 on the persistent grid. Integer tables; 60 hot rows
     at sample positions are the best items of a non-negative user group, whose
-    first-tier (rank 50) and safe (rank 68) thresholds both fall inside the hot
+    first-tier (rank 48) and safe (rank 68) thresholds both fall inside the hot
     scores: the group goes through every tier down to the -inf rescan. Checked:
     ~600 users from head, split-tail and last blocks plus 100 of the hot group
     against the exact top-1000 (lists and scores); then MMR over all 1M lists:
@@ -344,7 +344,7 @@ def test_config5_plan_1m_x_10m_k1000_then_mmr():
     U_n, I_n, d, k = 1_000_000, 10_000_000, 128, 1000
     plan = ops.score_topk_plan(U_n, I_n, torch.bfloat16, d, k)
     assert (plan["sample_stride"], plan["cap"], plan["user_blocks"]) == (32, 2048, 977), plan
-    assert (plan["first_tier_rank"], plan["sample_rank"]) == (50, 68), plan
+    assert (plan["first_tier_rank"], plan["sample_rank"]) == (48, 68), plan
     rng = np.random.default_rng(5005)
     users = _int_table_dev(U_n, d, 41)
     items = _int_table_dev(I_n, d, 42)
