@@ -136,12 +136,14 @@ constexpr int kFlushGap = DR_FLUSH_GAP;
 // 1.25M, where the survivor stream makes per-stage wave imbalance larger;
 // round 5: against two 64-KB slots -0.4 to -0.8 % at 10M, -0.35 to -0.65 % at
 // k = 1000, +0.1 % at 1.25M; three 48-KB slots +1 to +2.6 %). d <= 64 (its
-// LDS survivor staging needs room): two 48-KB slots, a barrier every 12 tiles
-// at d = 64 (round 5, against three 32-KB slots: -0.4 to -0.9 % at config 2,
-// -1.6 % at d = 32; four 24-KB slots +3.5 %; the stage margin of 384 keys puts
+// LDS survivor staging needs room): two 56-KB slots, a barrier every 14 tiles
+// at d = 64 (round 5, two 48-KB slots against three 32-KB: -0.4 to -0.9 % at
+// config 2, -1.6 % at d = 32; four 24-KB slots +3.5 %; 56 KB, with the
+// compaction histogram moved into the staging area, against 48 KB: -0.7 to
+// -1.7 % at config 2, -0.25 % at d = 32; the stage margin of 448 keys puts
 // k = 100 on CAP 1024 there). d = 256 spills with 64-KB stages.
 #ifndef DR_STAGE_BYTES_NARROW
-#define DR_STAGE_BYTES_NARROW 49152  // ring slot for d <= 64
+#define DR_STAGE_BYTES_NARROW 57344  // ring slot for d <= 64
 #endif
 constexpr int stage_bytes_for(int w) {
   return w == 128 ? DR_STAGE_BYTES_WIDE : (w <= 64 ? DR_STAGE_BYTES_NARROW : DR_STAGE_BYTES);
@@ -738,7 +740,11 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
   // user tile: the area must hold a whole wave's worth of blocks
   static_assert(!STAGED || SB >= 64, "staging area smaller than a wave");
   static_assert(!STAGED || NU_T * 32 <= 256, "staged slot field is 8 bits");
-  constexpr int WAVE_BYTES = UPW * 4 + 256 * 4 + SB * (64 + 8);
+  // The compaction's radix histogram (1 KB) shares the staging area: it is
+  // used only by check_compact, which runs after resolve() has emptied the
+  // staged blocks (stage ends, unit end).
+  constexpr int STAGE_AREA = SB * (64 + 8);
+  constexpr int WAVE_BYTES = UPW * 4 + (STAGE_AREA > 1024 ? STAGE_AREA : 1024);
   static_assert(RING_BYTES + kWaves * WAVE_BYTES <= 163840, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[RING_BYTES + kWaves * WAVE_BYTES];
 
@@ -763,7 +769,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
   char* wbase = smem + RING_BYTES + wave * WAVE_BYTES;
   uint32_t* ucnt = reinterpret_cast<uint32_t*>(wbase);
   uint32_t* hist = reinterpret_cast<uint32_t*>(wbase + UPW * 4);
-  float* blk_val = reinterpret_cast<float*>(wbase + UPW * 4 + 1024);  // [SB][16], 16-B aligned
+  float* blk_val = reinterpret_cast<float*>(wbase + UPW * 4);  // [SB][16], 16-B aligned
   // [SB] {tile of the unit | slot << 23 | h << 31, threshold bits}: one
   // ds_write_b64 per staged lane; 23 tile bits cover kMaxStagedRows (the host
   // refuses longer catalogs at the staged widths)
