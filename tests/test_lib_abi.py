@@ -146,6 +146,9 @@ def test_workspace_reflects_split_tail_plan():
     dense = (1_000_000 + 448) * (10_000_000 // 128 // 32) * 4
     with _backend.plan_knobs(scan_slots=256):
         assert dense <= lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100) < dense + 200_000_000
+    # a budget below the matrix (2 GiB) falls back to the compaction path's buffers
+    with _backend.plan_knobs(scan_slots=256, sample_dense=2):
+        assert lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100) < dense
     with _backend.plan_knobs(scan_slots=256, sample_dense=0):
         split = lib.dr_score_topk_workspace(1_000_000, 10_000_000, bf16, 128, 100)
         assert one + extra <= split < one + extra + 200_000_000
