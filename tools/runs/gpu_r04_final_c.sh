@@ -8,6 +8,6 @@ export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 cd $R
 bash tools/gpu_pmc_kernels.sh gather bpr fp32
-bash tools/gpu_r04_rehearse.sh
+bash tools/runs/gpu_r04_rehearse.sh
 mkdir -p gpurun_out/r04fc
 timeout -k 10 300 python3 bench.py > gpurun_out/r04fc/bench.jsonl 2> gpurun_out/r04fc/bench.err

@@ -11,4 +11,4 @@ bash tools/gpu_pmc_kernels.sh catalog score1m mmr gather bpr fp32
 bash tools/gpu_pmc_mfma.sh catalog score1m
 cp gpurun_out/pmck/pmc_*.json profiles/
 cp gpurun_out/pmcm/pmc_mfma_*.json profiles/
-bash tools/gpu_r04_final_a.sh
+bash tools/runs/gpu_r04_final_a.sh

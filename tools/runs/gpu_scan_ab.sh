@@ -1,6 +1,6 @@
 # Score-scan A/B (tools/variant_bench.py, outputs must be identical) at
 # config 2 (d=64, 1M x 1M), d=32 and the k=1000 shape; then the scan parity
-# tests. Usage: bash tools/gpu_scan_ab.sh product,VARIANT[,...] TAG
+# tests. Usage: bash tools/runs/gpu_scan_ab.sh product,VARIANT[,...] TAG
 set -e
 mkdir -p gpurun_out
 L=$1; T=$2

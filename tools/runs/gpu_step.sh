@@ -1,7 +1,7 @@
 #!/bin/bash
 # Parity suite (optionally a -k selection first), then the headline bench and
 # the named secondary workload lines, each under its own time limit; the first
-# failure ends the script.   usage: tools/gpu_step.sh [-k EXPR] [workload ...]
+# failure ends the script.   usage: tools/runs/gpu_step.sh [-k EXPR] [workload ...]
 set -e
 mkdir -p gpurun_out
 if [ "$1" = "-k" ]; then
