@@ -538,11 +538,14 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   p.n_users_pad = p.n_ublocks * p.users_per_wg;
   const int64_t slots = device_cus();
   const int64_t stage_items = stage_items_for(w);
-  // each chunk stays long enough to amortise its start (B fragments, ring fill)
-  const int64_t min_chunk = 65536;
   int max_c_override = 0;
   const int64_t B = p.n_ublocks;
   const int64_t H = (B / slots) * slots;
+  // each chunk stays long enough to amortise its start (B fragments, ring
+  // fill); a grid smaller than the CU count (H = 0) may split down to one
+  // stage per chunk: a catalog shorter than 2^16 rows (config 1: 943 users x
+  // 1682 items) otherwise ran on one CU, flooding its buffers from -inf
+  const int64_t min_chunk = H > 0 ? 65536 : std::min<int64_t>(65536, stage_items);
   if (H > 0 && !seedable) max_c_override = 1;
   const int64_t T = B - H;
   int best_c = 1;
