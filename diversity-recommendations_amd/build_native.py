@@ -39,6 +39,12 @@ CFLAGS = [
 ]
 
 
+# Per-source flags. ild.hip: MFMA results in VGPRs (the streamed ILD's
+# epilogue reads every Gram element once with VALU; AGPR results each need a
+# v_accvgpr_read first).
+FILE_FLAGS = {"ild.hip": ("-mllvm", "-amdgpu-mfma-vgpr-form")}
+
+
 def _headers_mtime() -> float:
     hs = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
     return max((h.stat().st_mtime for h in hs), default=0.0)
@@ -56,7 +62,8 @@ def _compile(src: Path, verbose: bool, obj_dir: Path = OBJ_DIR, extra=(), build_
     if same_flags and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime,
                                                                   _headers_mtime()):
         return obj
-    cmd = [HIPCC, *CFLAGS, *extra, *id_flags, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(src.name, ()), *extra, *id_flags, "-c", str(src), "-o",
+           str(obj)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -20,6 +20,10 @@ void set_error(const std::string& msg);
 // knob `id` holds a value (not NaN).
 bool plan_knob(int id, double* v);
 
+// Compute units of the current device (cached per device ordinal; 256 if the
+// query fails): the grid of the persistent kernels.
+int device_cus();
+
 #define DR_CHECK_ARG(cond, msg)                                   \
   do {                                                            \
     if (!(cond)) {                                                \

@@ -198,6 +198,7 @@ def dtype_code(dt: torch.dtype) -> int:
 PLAN_KNOBS = {
     "scan_slots": 0, "scan_split": 1, "tail_keys": 2, "scan_seed": 3,
     "guess_stride": 4, "guess_z1": 5, "guess_c1": 6, "guess_tight": 7, "sample_dense": 8,
+    "ild_stream": 9, "ild_bufs": 10,
 }
 
 

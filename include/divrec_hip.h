@@ -66,9 +66,17 @@ enum dr_plan_knob {
   DR_KNOB_GUESS_C1 = 6,     /* set: the offset c1 of that form (z defaults to 3) */
   DR_KNOB_GUESS_TIGHT = 7,  /* 0: one tier (ks1 = ks) */
   DR_KNOB_SAMPLE_DENSE = 8, /* 0: sample scan on compacted key buffers, not dense tile maxima; >1: budget GiB */
-  DR_KNOB_COUNT = 9
+  DR_KNOB_ILD_STREAM = 9,   /* dr_ild_embedding, k <= 128: 0 = one wave per user, 1 = streamed persistent grid */
+  DR_KNOB_ILD_BUFS = 10,    /* streamed ILD: ring slots (1-KB row pieces) per wave, at least one list's (default: as many as LDS allows) */
+  DR_KNOB_COUNT = 11
 };
-/* Set knob `knob` to `value` (NaN = default). DR_EINVAL for an unknown knob. */
+/* Set knob `knob` to `value` (NaN = default). DR_EINVAL for an unknown knob,
+ * an infinite value or one outside the knob's range: SCAN_SLOTS, SCAN_SPLIT,
+ * TAIL_KEYS and GUESS_STRIDE take integers in [1, 2^30]; SCAN_SEED, GUESS_TIGHT
+ * and ILD_STREAM 0 or 1; GUESS_Z1 / GUESS_C1 any finite value in [-64, 64];
+ * SAMPLE_DENSE 0 (off), 1 (on, the default budget) or a budget in GiB above
+ * 1 (up to 2^20); ILD_BUFS an
+ * integer in [1, 64]. */
 int dr_set_plan_knob(int knob, double value);
 /* Current value of a knob (NaN = default; NaN for an unknown knob). */
 double dr_get_plan_knob(int knob);

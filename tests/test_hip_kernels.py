@@ -716,6 +716,74 @@ def test_ild_embedding(d, k, kind):
     assert np.allclose(got, ref, rtol=2e-5, atol=2e-5 * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("d", [32, 64, 128])
+@pytest.mark.parametrize("k", [1, 2, 10, 31, 33, 64, 100, 128])
+@pytest.mark.parametrize("rec_dtype", [torch.int64, torch.int32])
+def test_ild_embedding_stream_matches_wave_per_user(d, k, rec_dtype):
+    """The streamed persistent-grid ILD (k <= 128, d <= 128; the default):
+    int64 and int32 lists, more users than the grid's waves (each wave's
+    pipeline runs many users, its last ones re-issued as padding), a ring of
+    one list's pieces, of 1.5 and 3 lists (ild_bufs) and the LDS-sized
+    default, which must agree bit for bit (the same arithmetic, only the
+    pipeline depth differs). Bad ids give NaN and count once per user. Against float64 and
+    against the one-wave-per-user kernel (ild_stream = 0, per-pair
+    epilogue; the streamed one sums each Gram column weighted, so the fp32
+    rounding differs) the bar is the usual rel 2e-5."""
+    rng = np.random.default_rng(d * 1000 + k)
+    E = oracle.as_bf16_f32(rng.standard_normal((5000, d)).astype(np.float32))
+    Et = _bf16(E)
+    nu = 3 * 1024 + 77  # > the 1024 waves of a 256-CU grid: several users per wave
+    recs = rng.integers(0, 5000, size=(nu, k))
+    recs[5, k // 2] = 5000  # out of range
+    recs[nu - 1, 0] = -1
+    rt = torch.from_numpy(recs).to(DEV, rec_dtype)
+    for kind in ("cosine", "dot", "euclidean"):
+        with _backend.plan_knobs(ild_stream=0):
+            base = ops.ild_embedding(rt, Et, kind, check=False).cpu().numpy()
+        first = None
+        ni = -(-k // (64 // (d // 8)))  # 1-KB pieces per list
+        for bufs in (None, ni, max(ni * 3 // 2, ni + 1), min(3 * ni, 64)):
+            err = torch.zeros(1, dtype=torch.int32, device=DEV)
+            with _backend.plan_knobs(**({} if bufs is None else {"ild_bufs": bufs})):
+                out = torch.empty(nu, dtype=torch.float32, device=DEV)
+                rc = _backend.lib().dr_ild_embedding(
+                    rt.data_ptr(), _backend.dtype_code(rec_dtype), nu, k, Et.data_ptr(), 5000, d,
+                    {"cosine": 0, "dot": 1, "euclidean": 2}[kind], out.data_ptr(), err.data_ptr(),
+                    _backend.stream(torch.device(DEV)))
+                assert rc == 0
+            got = out.cpu().numpy()
+            assert int(err.item()) == 2
+            assert np.isnan(got[5]) and np.isnan(got[nu - 1])
+            if first is None:
+                first = got
+            assert np.array_equal(got, first, equal_nan=True), (kind, bufs)
+            sc = np.nanmax(np.abs(base)) if k > 1 else 1.0
+            assert np.allclose(got, base, rtol=2e-5, atol=2e-5 * sc, equal_nan=True), (kind, bufs)
+        ok = np.ones(nu, bool)
+        ok[[5, nu - 1]] = False
+        ref = oracle.ild_embedding_f64(recs[ok][:300], E, kind)
+        if k == 1:
+            assert np.isnan(got[ok][:300]).all()  # 0 / 0, as the reference
+        else:
+            assert np.allclose(got[ok][:300], ref, rtol=2e-5, atol=2e-5 * np.abs(ref).max())
+
+
+def test_ild_embedding_stream_small_grids():
+    """Fewer users than waves (idle waves return at once), one user, and a
+    wave with exactly one user: the pipeline's padding re-issues that user."""
+    rng = np.random.default_rng(3)
+    E = oracle.as_bf16_f32(rng.standard_normal((700, 128)).astype(np.float32))
+    for nu in (1, 3, 1023, 1025):
+        recs = rng.integers(0, 700, size=(nu, 100))
+        rt = torch.from_numpy(recs).to(DEV)
+        got = ops.ild_embedding(rt, _bf16(E), "cosine").cpu().numpy()
+        with _backend.plan_knobs(ild_stream=0):
+            base = ops.ild_embedding(rt, _bf16(E), "cosine").cpu().numpy()
+        assert np.allclose(got, base, rtol=2e-5, atol=1e-6)
+        ref = oracle.ild_embedding_f64(recs[:50], E, "cosine")
+        assert np.allclose(got[:50], ref, rtol=2e-5, atol=1e-6)
+
+
 # --------------------------------------------------------------------------- BPR + Adam
 @pytest.mark.parametrize("d", [100, 128, 256])  # 100: the reference experiments' embedding_dim
 def test_bpr_fwd_bwd(d):

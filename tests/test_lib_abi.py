@@ -167,8 +167,8 @@ def test_plan_knobs_set_restore_and_no_environment(monkeypatch):
     import math
     lib = _backend.load_library()
     bf16 = _backend.DR_BF16
-    assert all(math.isnan(lib.dr_get_plan_knob(i)) for i in range(9))
-    assert lib.dr_set_plan_knob(9, 1.0) == -1  # DR_EINVAL: unknown knob
+    assert all(math.isnan(lib.dr_get_plan_knob(i)) for i in range(11))
+    assert lib.dr_set_plan_knob(11, 1.0) == -1  # DR_EINVAL: unknown knob
     out = (ctypes.c_int64 * 13)()
     assert lib.dr_score_topk_plan(1_000_000, 10_000_000, bf16, 128, 100, out, 13) == 0
     base = list(out)

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 6: streamed ILD with the next user's pieces interleaved between the
+# Gram tiles: parity tests, A/B against the one-wave-per-user kernel at the
+# config-4 shape (10M and 100K rows), k = 10, d = 64, euclidean; the diag
+# build's phase cycles per user.
+set -e
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r06ild9
+mkdir -p $O
+cd $R
+timeout -k 10 400 python3 -u -m pytest tests/test_hip_kernels.py -k "ild_embedding" -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1
+timeout -k 10 200 python3 -u tools/ild_ab.py --variants stream,ild_stream=0,diag1@stream --rounds 5 >> $O/ab.jsonl 2>> $O/ab.err || true
+timeout -k 10 200 python3 -u tools/ild_ab.py --variants stream,ild_stream=0 --items 100000 --rounds 3 >> $O/ab.jsonl 2>> $O/ab.err || true
+timeout -k 10 200 python3 -u tools/ild_ab.py --variants stream,ild_stream=0,diag1@stream --k 10 --rounds 3 >> $O/ab.jsonl 2>> $O/ab.err || true
+timeout -k 10 200 python3 -u tools/ild_ab.py --variants stream,ild_stream=0 --dim 64 --rounds 3 >> $O/ab.jsonl 2>> $O/ab.err || true
+timeout -k 10 200 python3 -u tools/ild_ab.py --variants stream,ild_stream=0 --kind euclidean --rounds 3 >> $O/ab.jsonl 2>> $O/ab.err || true
