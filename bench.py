@@ -86,6 +86,10 @@ def parse():
     ap.add_argument("--check-users", type=int, default=0,
                     help="after timing, recompute this many of each rank's final users "
                          "over the whole catalog on one device and require identical lists")
+    ap.add_argument("--fp64-check-users", type=int, default=1024,
+                    help="world size 1: check this many of the timed call's lists (head, "
+                         "split-tail and last user blocks) against float64 scores of the "
+                         "same tables (gap-aware rule; 0 = off)")
     ap.add_argument("--workload", default="catalog",
                     choices=["catalog", "score1m", "gather", "bpr", "mmr", "fp32", "ml100k",
                              "excl"])
@@ -508,7 +512,7 @@ def time_layout(args, world: int, dev, S: int, record_recs: bool = True):
             e[3].record()
             ev["topk0"].append(e[0]); ev["topk1"].append(e[1])
             ev["ild0"].append(e[2]); ev["ild1"].append(e[3])
-        return i, ild
+        return s, i, ild
 
     for _ in range(args.warmup):
         step(False)
@@ -517,7 +521,7 @@ def time_layout(args, world: int, dev, S: int, record_recs: bool = True):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        recs, ild = step(True)
+        scores, recs, ild = step(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -530,7 +534,8 @@ def time_layout(args, world: int, dev, S: int, record_recs: bool = True):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return {"lay": lay, "S": S, "dt": float(t[0]), "ild_max": float(t[1]),
             "topk_max": float(t[2]), "topk_s": topk_s, "users": users, "items": items,
-            "recs": recs if record_recs else None, "u_lo": u_lo, "u_hi": u_hi, "lo": lo, "hi": hi}
+            "recs": recs if record_recs else None, "scores": scores if record_recs else None,
+            "u_lo": u_lo, "u_hi": u_hi, "lo": lo, "hi": hi}
 
 
 def main():
@@ -566,6 +571,7 @@ def main():
     u_lo, u_hi, lo, hi = r["u_lo"], r["u_hi"], r["lo"], r["hi"]
 
     cfg_key = f"U{U_n}_I{I_n}_d{d}_k{k}_G{world}"
+    idb = r["recs"].element_size() if r["recs"] is not None else 4  # id bytes the ILD reads
     flops = 2.0 * (u_hi - u_lo) * (hi - lo) * d
     achieved = flops / r["topk_s"] / 1e12
     traffic = pmc_traffic("catalog", cfg_key, SCAN_KERNELS, per_step=0) or load_traffic(cfg_key)
@@ -592,10 +598,11 @@ def main():
             "item_shards": S,
         },
         "ild_users_per_s": U_n / r["ild_max"],
-        "ild_roofline": dict(_hbm(U_n // world * (k * 8 + k * d * 2 + 4), r["ild_max"],
-                                  pmc_traffic("catalog", cfg_key, "ild_embedding_regs")),
-                             kernel="dr_ild_embedding (cosine)",
-                             per_unit=f"{k * 8 + k * d * 2 + 4} B/user = k ids + k bf16 rows + out",
+        "ild_roofline": dict(_hbm(U_n // world * (k * idb + k * d * 2 + 4), r["ild_max"],
+                                  pmc_traffic("catalog", cfg_key, "ild_embedding_stream")),
+                             kernel="dr_ild_embedding (cosine; ild_embedding_stream)",
+                             per_unit=f"{k * idb + k * d * 2 + 4} B/user = k {8 * idb}-bit ids "
+                                      f"+ k bf16 rows + out",
                              # at k=100 report the MFMA side too (upper-triangle Gram)
                              mfma_tflops=U_n // world * k * (k - 1) * d / r["ild_max"] / 1e12,
                              mfma_frac=U_n // world * k * (k - 1) * d / r["ild_max"] / 1e12
@@ -620,6 +627,13 @@ def main():
     if args.check_users > 0:
         result["check"] = check_lists(args, r["lay"], r["users"], r["items"], r["recs"], u_lo,
                                       U_n, k, world)
+    elif world == 1 and args.fp64_check_users > 0:
+        # the timed call's own lists on its own tables, against float64
+        # (outside the timed region)
+        sel = check_user_sample(U_n, I_n, d, k, args.fp64_check_users)
+        result["check"] = fp64_gap_check(r["users"], r["items"], r["scores"], r["recs"], sel, k)
+        if not result["check"]["ok"]:
+            print(f"fp64 list check FAILED: {result['check']}", file=sys.stderr, flush=True)
     if world >= 4 and world % 2 == 0 and S != 2 and not args.no_alt_grid:
         # the (N/2) x 2 grid beside the main layout: same work,
         # 2-way item shards, users split N/2 ways
@@ -644,6 +658,73 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def check_user_sample(U_n: int, I_n: int, d: int, k: int, n: int) -> torch.Tensor:
+    """~n users of the call's plan (ops.score_topk_plan), drawn from every
+    kind of unit: whole-catalog head blocks, split-tail blocks and the last
+    (partial) block; sorted, unique."""
+    plan = ops.score_topk_plan(U_n, I_n, torch.bfloat16, d, k)
+    upw, head = plan["users_per_wg"], plan["head_blocks"]
+    g = torch.Generator().manual_seed(4242)
+    head_users = min(head * upw, U_n)
+    last0 = max((plan["user_blocks"] - 1) * upw, head_users)
+    ranges = [(0, head_users), (head_users, last0), (last0, U_n)]  # head, split tail, last block
+    want = [n * 3 // 8, n * 3 // 8, n - 2 * (n * 3 // 8)]
+    parts, carry = [], 0
+    for (lo, hi), w in zip(reversed(ranges), reversed(want)):  # last block first: it is small
+        m = min(w + carry, hi - lo)  # a short range hands its deficit to the next one
+        carry = w + carry - m
+        if m > 0:
+            parts.append(lo + torch.randperm(hi - lo, generator=g)[:m])
+    return torch.sort(torch.cat(parts)).values
+
+
+def fp64_gap_check(users: torch.Tensor, items: torch.Tensor, scores: torch.Tensor,
+                   recs: torch.Tensor, sel: torch.Tensor, k: int, chunk: int = 1 << 19,
+                   extra: int = 64) -> dict:
+    """The rule of tests/test_hip_kernels.py::test_score_topk_float_tolerance
+    on the timed call's own lists (bf16 tables: exact products, so only the
+    fp32 summation order separates a score from its float64 value):
+    every returned score within tol of its float64 value and the list sorted
+    within tol; every returned item at or above the exact k-th score - 2 tol;
+    every item scoring above the k-th + 2 tol returned. The exact float64
+    top-(k + extra) of each selected user over the whole catalog is built on
+    the device chunk by chunk (every item above the k-th score is among the
+    top k - 1, so it holds the whole must-return set)."""
+    dev = users.device
+    d = users.shape[1]
+    tol = 1e-5 * (d / 64) ** 0.5
+    sel = sel.to(dev)
+    U = users[sel].double()
+    got_i = recs[sel].long()
+    got_s = scores[sel].double()
+    best_s = torch.full((sel.numel(), k + extra), -float("inf"), dtype=torch.float64, device=dev)
+    best_i = torch.zeros((sel.numel(), k + extra), dtype=torch.int64, device=dev)
+    t0 = time.perf_counter()
+    for c0 in range(0, items.shape[0], chunk):
+        S = U @ items[c0:c0 + chunk].double().T
+        ts, ti = torch.topk(S, min(k + extra, S.shape[1]), dim=1)
+        best_s, pos = torch.topk(torch.cat([best_s, ts], 1), k + extra, dim=1)
+        best_i = torch.gather(torch.cat([best_i, ti + c0], 1), 1, pos)
+        del S
+    exact = (U.unsqueeze(1) * items[got_i.clamp(min=0)].double()).sum(-1)  # float64 score per item
+    kth = best_s[:, k - 1:k]
+    ok_score = bool(((got_s - exact).abs() <= tol).all())
+    ok_sorted = bool((got_s[:, 1:] - got_s[:, :-1] <= 2 * tol).all())
+    ok_above = bool((exact >= kth - 2 * tol).all())
+    must = best_s > kth + 2 * tol
+    hit = (best_i.unsqueeze(2) == got_i.unsqueeze(1)).any(2)
+    ok_must = bool((hit | ~must).all())
+    ok_valid = bool((got_i >= 0).all())
+    exact_order = int((best_i[:, :k] != got_i).any(1).sum())
+    return {"users_checked": int(sel.numel()), "rule": "fp64 gap-aware", "tol": tol,
+            "ok": ok_score and ok_sorted and ok_above and ok_must and ok_valid,
+            "scores_within_tol": ok_score, "sorted_within_tol": ok_sorted,
+            "all_above_kth_minus_2tol": ok_above, "all_clear_top_k_returned": ok_must,
+            "users_not_in_exact_float64_order": exact_order,
+            "max_abs_score_err": float((got_s - exact).abs().max()),
+            "check_s": time.perf_counter() - t0}
 
 
 def check_lists(args, lay, users, items, recs, u_lo, U_n, k, world):

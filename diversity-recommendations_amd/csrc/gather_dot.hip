@@ -51,9 +51,7 @@ struct Vec16<__bf16> {
 };
 
 constexpr int kUnroll = 4;
-#ifndef DR_GATHER_UW
-#define DR_GATHER_UW 8  // pairs in flight per lane group when a lane holds one 16-B row chunk
-#endif
+constexpr int kGatherUW = 8;  // pairs in flight per lane group when a lane holds one 16-B row chunk
 constexpr int kBlock = 256;
 
 __device__ __forceinline__ bool in_rows(int64_t r, int64_t n) { return r >= 0 && r < n; }
@@ -279,7 +277,7 @@ int launch_fwd(const T* U, int64_t nu, const T* I, int64_t ni, int64_t d, const 
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, U, nu, I, ni, d, (int)chunks, uid,
                        iid, n, out, err);
   };
-  constexpr int UW = DR_GATHER_UW;  // pairs in flight per group (rows held raw: 4 registers per chunk)
+  constexpr int UW = kGatherUW;  // pairs in flight per group (rows held raw: 4 registers per chunk)
 #define DR_RUNS(GG, CC)                                                                       \
   (chunks == GG * CC                                                                           \
        ? go(gather_dot_runs<T, GG, CC, false, (GG >= UW && CC == 1) ? UW : 4>, GG)             \

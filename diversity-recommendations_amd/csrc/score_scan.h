@@ -11,8 +11,9 @@
 //   * Each wave keeps the rows of its NU_T*32 users resident in registers as
 //     MFMA B fragments for the whole scan.
 //   * Item rows go HBM -> LDS by LDS-DMA (global_load_lds_dwordx4) into a ring
-//     of stages (W = 128: two 64-KB slots, one stage ahead; else three
-//     32-KB slots, two ahead), one s_barrier per stage; the LDS image is
+//     of stages (W = 128: two 72-KB slots, one stage ahead; W <= 64: two
+//     56-KB slots; W >= 256: three 32-KB slots, two ahead), one s_barrier per
+//     stage; the LDS image is
 //     XOR-swizzled through the per-lane source address so the A-fragment
 //     ds_read_b128s are bank-conflict-free. All 8 waves share every stage.
 //     A fragments are read two k-steps ahead of the MFMAs that use them.
@@ -58,78 +59,38 @@ enum {
   kDgNTiles, kDgNEnqueue, kDgNDrain, kDgNFlush, kDgNStages, kDgRealtime, kDgSlots = 16
 };
 
-// Geometry knobs. The defaults are the product configuration; the -D
-// overrides exist so tools/variant_bench.py can time alternatives side by side
-// (build_native.py --variant NAME -D KEY=VAL).
-#ifndef DR_STAGE_BYTES
-#define DR_STAGE_BYTES 32768  // one LDS ring slot, d != 128
-#endif
-#ifndef DR_RING
-#define DR_RING 3  // ring slots (RING - 1 stages in flight), d != 128
-#endif
+// Geometry. Every alternative measured against these values lost and was
+// removed (DESIGN.md §3.1, A/B records under profiles/): one wave per SIMD
+// (rounds 2 and 5), 12 / 16 waves at d <= 64, SIMD-pair priorities, two
+// accumulator sets in ping-pong, the A fragments read per half chain, other
+// stage sizes, slacks and flush gaps. The one -D knob kept is the d = 128
+// stage size (DR_STAGE_BYTES_WIDE: its L2-reuse / time trade-off is
+// re-measured with PMC FETCH beside the time, profiles/r06/stage_fetch/).
 #ifndef DR_STAGE_BYTES_WIDE
 #define DR_STAGE_BYTES_WIDE 73728  // ring slot for d = 128 (9 tiles: 72 KB; 64 KB measured +0.4-0.8 %)
 #endif
-#ifndef DR_RING_WIDE
-#define DR_RING_WIDE 2  // ring slots for d = 128
-#endif
-#ifndef DR_NUT
-#define DR_NUT 4  // user tiles of 32 per wave for d = 128
-#endif
-#ifndef DR_NUT_NARROW
-#define DR_NUT_NARROW 8  // user tiles of 32 per wave for d <= 64 (measured: 8 is +14 % at d=64, 1M x 1M)
-#endif
-#ifndef DR_PRIO
-#define DR_PRIO 0  // static s_setprio 1 for waves 4-7 (measured: no gain)
-#endif
-#ifndef DR_DYNPRIO
-#define DR_DYNPRIO 0  // s_setprio 1 around each tile's MFMA issue (A/B knob)
-#endif
-#ifndef DR_APIPE
-#define DR_APIPE 1  // A fragments read two k-steps ahead
-#endif
-#ifndef DR_FLUSH_GAP
-#define DR_FLUSH_GAP 96  // new keys a buffer takes past k + kSlack before compaction
-#endif
-#ifndef DR_ENQ_STAGED
-// survivors: 0 = direct per-lane enqueue, 1 = stage lane blocks in LDS and
-// resolve them per stage, 2 = staged for d <= 64 only (measured: staged is 4%
-// faster at d=64, where survivors per MFMA are twice as dense, and 4% slower
-// at d=128)
-#define DR_ENQ_STAGED 2
-#endif
-#ifndef DR_ENQ_FAST
-#define DR_ENQ_FAST 1  // direct enqueue: one-survivor lanes store their max (no value select)
-#endif
-#ifndef DR_STAGE_BLOCKS
-#define DR_STAGE_BLOCKS 64  // staged lane blocks per wave (>= 64: one user tile always fits)
-#endif
-#ifndef DR_RESOLVE_BATCHED
-#define DR_RESOLVE_BATCHED 1  // staged blocks: one LDS slot reservation per block, not per score
-#endif
-#ifndef DR_COMPACT_INLINE
-#define DR_COMPACT_INLINE __noinline__
-#endif
+constexpr int kStageBytesOther = 32768;  // ring slot for d = 256 / 512 (three slots)
+constexpr int kRingOther = 3;
+constexpr int kRingWide = 2;          // d = 128: two slots, one stage ahead
+constexpr int kNutWide = 4;           // user tiles of 32 per wave for d = 128
+constexpr int kNutNarrow = 8;         // for d <= 64 (+14 % at d = 64, 1M x 1M, against 4)
+constexpr int kFlushGapDefault = 96;  // new keys a buffer takes past k + kSlack before compaction
+// Survivors are staged in LDS and resolved per stage for d <= 64 (twice as
+// dense per MFMA there: 4 % faster), stored directly for d >= 128 (4 %
+// faster there).
+constexpr int kStageBlocks = 64;  // staged lane blocks per wave (>= 64: one user tile always fits)
 
-#ifndef DR_WAVES
-#define DR_WAVES 8  // 8: two waves per SIMD (256 registers each); 4: one per SIMD (512)
-#endif
-#ifndef DR_WAVES_NARROW
-#define DR_WAVES_NARROW DR_WAVES  // waves per workgroup for rows of <= 128 bytes (d <= 64 bf16)
-#endif
-// Waves per workgroup of a scan over rows of w bf16 units (one workgroup per
-// CU): the register budget per wave is 512 / (waves / 4) VGPRs.
-constexpr int waves_for(int w) { return w <= 64 ? DR_WAVES_NARROW : DR_WAVES; }
-constexpr int kMaxWaves = DR_WAVES > DR_WAVES_NARROW ? DR_WAVES : DR_WAVES_NARROW;
+// Waves per workgroup of a scan (one workgroup per CU): two per SIMD, 256
+// VGPRs each.
+constexpr int kWavesScan = 8;
+constexpr int waves_for(int) { return kWavesScan; }
+constexpr int kMaxWaves = kWavesScan;
 // Longest catalog a staged (W <= 64) scan takes: its staged blocks name their
 // tile in 23 bits (dr_score_topk refuses longer ones).
 constexpr int64_t kMaxStagedRows = (int64_t)32 << 23;
 constexpr int kTileItems = 32;
-#ifndef DR_SLACK
-#define DR_SLACK 32
-#endif
-constexpr int kSlack = DR_SLACK;  // keys kept beyond k by a compaction
-constexpr int kFlushGap = DR_FLUSH_GAP;
+constexpr int kSlack = 32;  // keys kept beyond k by a compaction
+constexpr int kFlushGap = kFlushGapDefault;
 
 // Stage geometry per row width. d = 128: two 72-KB slots (one barrier per
 // 9 tiles; measured against three 32-KB slots: +2 % at 10M items, +6 % at
@@ -142,16 +103,12 @@ constexpr int kFlushGap = DR_FLUSH_GAP;
 // compaction histogram moved into the staging area, against 48 KB: -0.7 to
 // -1.7 % at config 2, -0.25 % at d = 32; the stage margin of 448 keys puts
 // k = 100 on CAP 1024 there). d = 256 spills with 64-KB stages.
-#ifndef DR_STAGE_BYTES_NARROW
-#define DR_STAGE_BYTES_NARROW 57344  // ring slot for d <= 64
-#endif
+constexpr int kStageBytesNarrow = 57344;  // ring slot for d <= 64
 constexpr int stage_bytes_for(int w) {
-  return w == 128 ? DR_STAGE_BYTES_WIDE : (w <= 64 ? DR_STAGE_BYTES_NARROW : DR_STAGE_BYTES);
+  return w == 128 ? DR_STAGE_BYTES_WIDE : (w <= 64 ? kStageBytesNarrow : kStageBytesOther);
 }
-#ifndef DR_RING_NARROW
-#define DR_RING_NARROW 2  // ring slots for d <= 64
-#endif
-constexpr int ring_for(int w) { return w == 128 ? DR_RING_WIDE : (w <= 64 ? DR_RING_NARROW : DR_RING); }
+constexpr int kRingNarrow = 2;  // ring slots for d <= 64
+constexpr int ring_for(int w) { return w == 128 ? kRingWide : (w <= 64 ? kRingNarrow : kRingOther); }
 
 template <int D>  // D = W, the row's width in bf16 units (row bytes / 2)
 struct TileGeom {
@@ -180,26 +137,9 @@ struct TileGeom {
 // most four against each item tile, one accumulator set (4*16 VGPRs) reused
 // by the groups, so narrow rows can hold more users per wave.
 constexpr int nut_for(int w) {
-  return w >= 512 ? 1 : (w >= 256 ? 2 : (w <= 64 ? DR_NUT_NARROW : DR_NUT));
+  return w >= 512 ? 1 : (w >= 256 ? 2 : (w <= 64 ? kNutNarrow : kNutWide));
 }
-#ifndef DR_UTPIPE
-// Software-pipelined epilogue per user tile (the main scans; sample scans keep
-// the group epilogue): the MFMA chain of each (item tile, user tile) job goes
-// to one of two accumulators, and the hot test of the previous job runs right
-// after the next job's chain is issued, i.e. under this wave's own MFMAs.
-#define DR_UTPIPE 1
-#endif
-#ifndef DR_PINGPONG
-// Two user-tile groups with one accumulator set EACH, software-pipelined: the
-// epilogue of one group runs while the other group's MFMAs execute (the wave
-// issues VALU under its own MFMAs), instead of both groups sharing one set
-// and every epilogue waiting for the MFMA chain before it. Needs NU_T <= 6
-// (two sets of NU_T/2 tiles = 96 VGPRs beside 96 of B fragments).
-#define DR_PINGPONG 0
-#endif
-constexpr int ngroup_for(int w) {
-  return (nut_for(w) > 4 || (DR_PINGPONG && w <= 64)) ? nut_for(w) / 2 : nut_for(w);
-}
+constexpr int ngroup_for(int w) { return nut_for(w) > 4 ? nut_for(w) / 2 : nut_for(w); }
 template <int V>
 struct IC {
   static constexpr int value = V;
@@ -345,23 +285,16 @@ __device__ __forceinline__ float max16(const f32x16& a) {
   return m;
 }
 
-#ifndef DR_HOT_MAXIMUM
-#define DR_HOT_MAXIMUM 1  // hot test on v_maximum3_f32 (0: the maxNum chain above)
-#endif
 // The hot test's max: IEEE-754-2019 maximum (gfx950 v_maximum3_f32: NaN
 // propagates, no operand canonicalisation), 8 VALU per tile instead of 10.
 // Only ever compared through hot(): a NaN max counts as a hit, so the exact
 // per-score tests behind it see the tile (NaN scores are never admitted there,
 // as with maxNum, where they were skipped by the max).
 __device__ __forceinline__ float hot_max16(const f32x16& a) {
-#if DR_HOT_MAXIMUM
   float m = __builtin_elementwise_maximum(a[0], a[1]);
 #pragma unroll
   for (int r = 2; r < 16; ++r) m = __builtin_elementwise_maximum(m, a[r]);
   return m;
-#else
-  return max16(a);
-#endif
 }
 // "some score of the tile may beat thr": a superset of `max > thr` (NaN = hit)
 __device__ __forceinline__ bool hot(float m, float thr) { return !(m <= thr); }
@@ -385,7 +318,7 @@ struct CompactResult {
 // 2048, k up to 1024) made the callee clobber so many registers that the
 // caller spilled its B fragments inside the MFMA loop (5x slower tiles).
 template <int P>
-__device__ DR_COMPACT_INLINE CompactResult compact_buffer_chunked(uint64_t* __restrict__ buf, int n_in, int k,
+__device__ __noinline__ CompactResult compact_buffer_chunked(uint64_t* __restrict__ buf, int n_in, int k,
                                                      int slack, const int32_t* __restrict__ ex,
                                                      int exn, uint32_t* __restrict__ hist) {
   constexpr int CH = 64 * P;
@@ -503,7 +436,7 @@ __device__ DR_COMPACT_INLINE CompactResult compact_buffer_chunked(uint64_t* __re
 // (the chunked form measured slower at d = 64, and letting it keep chunk 0
 // in registers spilled the d = 64 tile loop).
 template <int P>
-__device__ DR_COMPACT_INLINE CompactResult compact_buffer_resident(uint64_t* __restrict__ buf, int n_in, int k,
+__device__ __noinline__ CompactResult compact_buffer_resident(uint64_t* __restrict__ buf, int n_in, int k,
                                                      int slack, const int32_t* __restrict__ ex,
                                                      int exn, uint32_t* __restrict__ hist) {
   const int lane = dr::lane_id();
@@ -734,8 +667,8 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
   constexpr int RING_BYTES = kRing * kStageBytes;
   // per wave: per-user key counts, radix histogram, staged survivor blocks
   // (16 scores + one 8-B record: tile | slot | h, threshold)
-  constexpr bool STAGED = DR_ENQ_STAGED == 1 || (DR_ENQ_STAGED == 2 && D <= 64);
-  constexpr int SB = STAGED ? DR_STAGE_BLOCKS : 0;
+  constexpr bool STAGED = D <= 64;
+  constexpr int SB = STAGED ? kStageBlocks : 0;
   // stage_hits resolves a full stage area, then stages up to 64 lanes of one
   // user tile: the area must hold a whole wave's worth of blocks
   static_assert(!STAGED || SB >= 64, "staging area smaller than a wave");
@@ -760,12 +693,6 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5;
   const int col = lane & 31;
-#if DR_PRIO
-  // The second-dispatched half of the workgroup loses VALU arbitration to its
-  // SIMD partner on every segment; one static priority bump evens the pair
-  // (cdna_hip_programming.md T5, static form). Wave-uniform by readfirstlane.
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
   char* wbase = smem + RING_BYTES + wave * WAVE_BYTES;
   uint32_t* ucnt = reinterpret_cast<uint32_t*>(wbase);
   uint32_t* hist = reinterpret_cast<uint32_t*>(wbase + UPW * 4);
@@ -870,7 +797,6 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
       const uint32_t tb = lds_ring + ((t / SR) % kRing) * kStageBytes + (t % SR) * G::TILE_BYTES;
 #pragma unroll
       for (int ut = 0; ut < NG; ++ut) acc[ut] = f32x16{};
-#if DR_APIPE
       // Fragment s is read two k-steps before its MFMAs; each wait retires
       // exactly the fragment the next MFMAs consume.
       u32x4 af[KS];
@@ -883,19 +809,6 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
         if (s + 2 < KS) af[s + 2] = ds_read_b128_asm(tb + a_off(s + 2));
         kstep_mma<F32, NG>(af[s], bfr, g0, s, acc);
       }
-#else
-      constexpr int HALF = KS >= 4 ? KS / 2 : KS;
-#pragma unroll
-      for (int s0 = 0; s0 < KS; s0 += HALF) {
-        u32x4 af[HALF];
-#pragma unroll
-        for (int s = 0; s < HALF; ++s) af[s] = ds_read_b128_asm(tb + a_off(s0 + s));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int s = 0; s < HALF; ++s) kstep_mma<F32, NG>(af[s], bfr, g0, s0 + s, acc);
-      }
-#endif
     };
 
     // -------------------------------------------------------------- cold paths
@@ -986,7 +899,6 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
         mask &= vmask;
         const int slot = (g0 + ut) * 32 + col;
         uint64_t* ubuf = cbase + (size_t)slot * CAP;  // this lane's user buffer
-#if DR_ENQ_FAST
         // Common case: every hitting lane holds ONE survivor. It is then the
         // lane's maximum (all other scores are <= thr < it), so one round
         // stores it without the 16-way value select. Full tiles only (the
@@ -1004,7 +916,6 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
           }
           continue;
         }
-#endif
         while (__ballot(mask != 0u) != 0ull) {
           const bool has = mask != 0u;
           const int r = has ? __builtin_ctz(mask) : 0;
@@ -1251,7 +1162,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
         if (any != 0ull) stage_hits(t, acc, hb, GI);
         // end of a stage: resolve the staged blocks, compact full buffers
         if (last_group && ((t + 1) % SR == 0 || t + 1 == ntiles)) {
-          if (nblk > 0) resolve(IC<DR_RESOLVE_BATCHED>{});
+          if (nblk > 0) resolve(IC<1>{});
           check_compact(flush_at, a.slack);
         }
       } else {
@@ -1262,7 +1173,8 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
       }
     };
     // -------------------------------------------------- per-user-tile pipeline
-    // (DR_UTPIPE, the main scans): a job is one (item tile t, user tile u)
+    // (rows of <= 128 bytes: the main scans and the narrow GMAX sample scans,
+    // whose job test is gmax_ut): a job is one (item tile t, user tile u)
     // pair, KS k-steps into ONE accumulator (a single accumulation chain of
     // v_mfma_f32_32x32x16_bf16 issues at full rate). Jobs run t-major; job
     // (t, u) writes accumulator u % 2, and its hot test runs right after job
@@ -1276,7 +1188,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
     // Rows of <= 128 bytes only: at d = 128 (the headline) it measured +0.4 %
     // (a chain of 8 k-steps already covers the group's hot test), and the fp32
     // d = 128 / bf16 d = 256 instances spill in the loop with it.
-    constexpr bool UTP = DR_UTPIPE && NU_T % 2 == 0 && W <= 64;
+    constexpr bool UTP = NU_T % 2 == 0 && W <= 64;
     auto read_a = [&](int t, u32x4 (&af)[KS]) {
       const uint32_t tb = lds_ring + ((t / SR) % kRing) * kStageBytes + (t % SR) * G::TILE_BYTES;
 #pragma unroll
@@ -1428,7 +1340,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
     };
     auto stage_end_utp = [&]() {
       if constexpr (STAGED) {
-        if (nblk > 0) resolve(IC<DR_RESOLVE_BATCHED>{});
+        if (nblk > 0) resolve(IC<1>{});
       }
       if (GMAX && a.gmax == 2) return;  // dense tile maxima: no buffers
       check_compact(flush_at, a.slack);
@@ -1467,50 +1379,6 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
         test_job(ntiles - 1, acc1, IC<NU_T - 1>{});
         stage_end_utp();
       }
-    } else if constexpr (DR_PINGPONG && NGRP == 2) {
-      // Ping-pong: tile t's group-0 MFMAs are issued, then group 1's epilogue
-      // of tile t-1 runs under them; group 1's MFMAs of tile t are issued,
-      // then group 0's epilogue of tile t runs under them. The stage-end work
-      // (resolve, compaction) follows group 1's epilogue of a stage's last
-      // tile, so both groups are complete through the stage when it runs; a
-      // user still gets at most one stage of keys between two compactions.
-      f32x16 acc0[NG], acc1[NG];
-      auto stage_end = [&](int t_last, int lim) {
-        if constexpr (STAGED) {
-          if (nblk > 0) resolve(IC<DR_RESOLVE_BATCHED>{});
-        }
-        check_compact(lim, a.slack);
-        (void)t_last;
-      };
-      auto epi = [&](int t, f32x16 (&acc)[NG], auto GI) {
-        DG_T0(t_h);
-        uint64_t hb[NG];
-        const uint64_t any = any_hits(acc, hb, GI);
-        DG_ADD(kDgHits, t_h);
-        if (any != 0ull) {
-          if constexpr (STAGED) stage_hits(t, acc, hb, GI);
-          else enqueue(t, acc, hb, GI);
-        }
-      };
-      for (int t = 0; t < ntiles; ++t) {
-        DG_CNT(kDgNTiles);
-        if (t % SR == 0) boundary(t / SR);
-        DG_T0(t_m);
-        mma_tile(t, acc0, IC<0>{});
-        DG_ADD(kDgMma, t_m);
-        if (t > 0) {
-          epi(t - 1, acc1, IC<1>{});
-          if (t % SR == 0) stage_end(t - 1, flush_at);
-        }
-        DG_T0(t_m2);
-        mma_tile(t, acc1, IC<1>{});
-        DG_ADD(kDgMma, t_m2);
-        epi(t, acc0, IC<0>{});
-      }
-      if (ntiles > 0) {
-        epi(ntiles - 1, acc1, IC<1>{});
-        stage_end(ntiles - 1, flush_at);
-      }
     } else {
     // One accumulator set: the partner wave on the same SIMD issues its MFMAs
     // while this wave runs the epilogue (two waves per SIMD by design).
@@ -1519,24 +1387,12 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
       DG_CNT(kDgNTiles);
       if (t % SR == 0) boundary(t / SR);
       DG_T0(t_m);
-#if DR_DYNPRIO
-      __builtin_amdgcn_s_setprio(1);  // MFMA issue wins the SIMD over the partner's epilogue
-#endif
       mma_tile(t, acc, IC<0>{});
-#if DR_DYNPRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
       DG_ADD(kDgMma, t_m);
       epilogue(t, acc, IC<0>{});
       if constexpr (NGRP > 1) {
         DG_T0(t_m2);
-#if DR_DYNPRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
         mma_tile(t, acc, IC<1>{});
-#if DR_DYNPRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
         DG_ADD(kDgMma, t_m2);
         epilogue(t, acc, IC<1>{});
       }

@@ -488,28 +488,18 @@ int cap_for(int w, int k) {
 }
 
 constexpr int kMaxTailChunks = 16;
-#ifndef DR_LONG_FLUSH
-#define DR_LONG_FLUSH 1  // 0: long lists flush at k + kSlack + kFlushGap (A/B only)
-#endif
+constexpr bool kLongFlush = true;  // long lists flush at CAP - margin, not k + kSlack + kFlushGap
 // Compaction slack and flush gap of the sample scan (ks <= ~70 keys per user).
-#ifndef DR_SAMPLE_SLACK
-#define DR_SAMPLE_SLACK 32
-#endif
-#ifndef DR_SAMPLE_GAP
-#define DR_SAMPLE_GAP 96
-#endif
-#ifndef DR_SAMPLE_GMAX
-#define DR_SAMPLE_GMAX 1  // sample scans keep tile maxima (TopkArgs::gmax); 0: every survivor
-#endif
-constexpr int kSampleSlack = DR_SAMPLE_SLACK;
-constexpr int kSampleGap = DR_SAMPLE_GAP;
+constexpr int kSampleSlackDefault = 32;
+constexpr int kSampleGapDefault = 96;
+constexpr int kSampleGmax = 1;  // sample scans keep tile maxima (TopkArgs::gmax)
+constexpr int kSampleSlack = kSampleSlackDefault;
+constexpr int kSampleGap = kSampleGapDefault;
 // The finalize of a split-tail user sorts every chunk's end-compacted keys
 // (<= k + kSlack each) in one wave; at most 1024 of them keeps its sort at
 // P = 16 (a 2048-key sort costs ~6x the 512-key one of a whole-catalog user).
 constexpr int kMaxTailKeys = 1024;
-#ifndef DR_HEAD_KEEP
-#define DR_HEAD_KEEP 1  // long lists: whole-catalog units end compacted to 1024 keys (0: A/B off)
-#endif
+constexpr bool kHeadKeep = true;  // long lists: whole-catalog units end compacted to 1024 keys
 
 // Grid tail: U users make B = ceil(U / UPWG) user blocks for `slots`
 // workgroups. Whole-catalog units run in ceil(B / slots) rounds, the last one
@@ -580,7 +570,7 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   // survivors (the guess's rank): with the flush at k + 128 = 1128 every user
   // compacted a ~1.1K-key buffer 3-4 times in the last third of the catalog;
   // at CAP - margin = 1792 most users never compact.
-  p.gap = head_flush > kMaxTailKeys && DR_LONG_FLUSH ? p.cap - (int)stage_items - k - kSlack
+  p.gap = head_flush > kMaxTailKeys && kLongFlush ? p.cap - (int)stage_items - k - kSlack
                                                      : kFlushGap;
   // a tail chunk ends with at most end_keep >= k keys, so c of them fit the
   // finalize's max_keys
@@ -589,7 +579,7 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   // with a compaction to at most kMaxTailKeys keys (slack kMaxTailKeys - k), so
   // the finalize sorts 1024 keys per user instead of 2048 (k = 1000: the
   // 2048-key sort cost ~24 ms per 1M users).
-  p.head_keep = DR_HEAD_KEEP && head_flush > kMaxTailKeys && k + 8 <= kMaxTailKeys ? kMaxTailKeys : 0;
+  p.head_keep = kHeadKeep && head_flush > kMaxTailKeys && k + 8 <= kMaxTailKeys ? kMaxTailKeys : 0;
   p.buf_rows = p.n_users_pad + (int64_t)(best_c - 1) * (B - p.n_head) * p.users_per_wg;
   const int64_t units = p.n_head + (B - p.n_head) * best_c;
   p.grid = (int)(units < slots ? units : slots);
@@ -618,13 +608,13 @@ int tail_keys(const Plan& p, int w, int k) {
   return n > 256 ? n : 256;
 }
 
-// Guessed thresholds (DR_GUESS). A scan that starts at -inf stores every
+// Guessed thresholds (kGuess). A scan that starts at -inf stores every
 // running top-k record of a user: ~k * (1 + ln(I / k)) keys, the survivor
 // stream that dominates short catalogs (47 % of wave time at d=64 over 1M
 // items). Instead a first scan over a strided sample of S = I / kGuessStride
 // rows keeps each user's ks best, and the main scan starts from just below the
 // ks-th best sample score. ks is the mean number of the user's true top k
-// inside the sample plus DR_GUESS_SIGMA standard deviations (+3), so for
+// inside the sample plus kGuessSigma standard deviations (+3), so for
 // exchangeable catalogs the guess is below the true k-th best score for all
 // but ~1e-8 of users. The guess is verified, not trusted: the finalize
 // appends every user left with fewer than k keys to a fail list, and those
@@ -641,21 +631,15 @@ struct Guess {
   int ks1 = 0;         // first-tier rank (<= ks): the main scan's threshold
 };
 
-#ifndef DR_GUESS
-#define DR_GUESS 1
-#endif
-#ifndef DR_GUESS_SIGMA
-#define DR_GUESS_SIGMA 6.0
-#endif
-#ifndef DR_GUESS_STRIDE
-#define DR_GUESS_STRIDE 32
-#endif
+constexpr bool kGuess = true;  // guessed thresholds for catalogs of >= 2^18 rows
+constexpr double kGuessSigma = 6.0;
+constexpr int kGuessStrideDefault = 32;
 // Two-tier guess (round 3): the main scan starts from the sample's
 // ks1-th best score; the users it fails are rescanned from their safe
 // (6-sigma) threshold by a second-tier scan spread over every CU, and the
 // rare users that fail that too by the whole-catalog rescan from -inf.
 // ks1 (round 5) is the smallest rank whose Poisson(mu) tail P(X >= ks1) is at
-// most DR_GUESS_TAIL = 0.5 % (the share of users expected to fail it); the
+// most kGuessTail = 0.5 % (the share of users expected to fail it); the
 // round-3 rule mu + 3 sigma + 1 had tails of 0.12-0.15 %. Measured with the
 // z knob giving the same ranks (profiles/r05/ab19/, ab20/, lists identical):
 // config 2 (ks1 10 -> 9) -1.05 %, d = 32 -2.7 %, an 8-way shard's 1.25M rows
@@ -670,32 +654,26 @@ int poisson_tail_rank(double mu, double tail) {
   }
   return 4096;
 }
-#ifndef DR_GUESS_TAIL
-#define DR_GUESS_TAIL 0.005
-#endif
+constexpr double kGuessTail = 0.005;
 constexpr int kMaxRescanChunks = 64;  // catalog chunks per user block of a second-tier rescan
-constexpr int64_t kGuessStride = DR_GUESS_STRIDE;
+constexpr int64_t kGuessStride = kGuessStrideDefault;
 constexpr int64_t kGuessMinItems = 1 << 18;
-#ifndef DR_GUESS_MAX_LOG2
-#define DR_GUESS_MAX_LOG2 23  // measured: +1.7 % at 5M rows, -0.3 % at 10M
-#endif
-constexpr int64_t kGuessMaxItems = 1ll << DR_GUESS_MAX_LOG2;
+constexpr int kGuessMaxLog2 = 23;  // measured: +1.7 % at 5M rows, -0.3 % at 10M
+constexpr int64_t kGuessMaxItems = 1ll << kGuessMaxLog2;
 // Long lists pay a survivor stream of ~k (1 + ln(I / k)) keys per user from
 // -inf (10K keys at k = 1000 over 10M items: 3.5x the k = 100 scan), which the
 // guess removes at any catalog length.
-#ifndef DR_GUESS_LONG_K
-#define DR_GUESS_LONG_K 256
-#endif
+constexpr int kGuessLongK = 256;
 
 // A plan with a split tail is always seeded (from kGuessMinItems rows): an
 // unseeded chunk pays the survivor stream of its own catalog part from -inf,
 // ~c times the keys of one whole-catalog pass for its users.
 Guess guess_for(int64_t n_items, int k, bool split_tail) {
   Guess g;
-  if (!DR_GUESS || n_items < kGuessMinItems) return g;
+  if (!kGuess || n_items < kGuessMinItems) return g;
   const int force = knob_int(DR_KNOB_SCAN_SEED, -1);  // A/B knob: 0 never, 1 always
   if (force == 0) return g;
-  if (n_items > kGuessMaxItems && k < DR_GUESS_LONG_K && !split_tail && force != 1) return g;
+  if (n_items > kGuessMaxItems && k < kGuessLongK && !split_tail && force != 1) return g;
   // Long catalogs sample more sparsely: the sample scan starts from -inf and
   // is survivor-dense (~1.5x the per-row cost of the seeded scan), so about
   // 2^16 sample rows are kept (stride 32 up to 2^22 rows, 64 from 4.2M,
@@ -703,16 +681,16 @@ Guess guess_for(int64_t n_items, int k, bool split_tail) {
   // stride 32 / 64 / 128 / 256 = 1912 / 1879 / 1873 / 1880 ms
   // (profiles/r02_scan/ab_stride_10m.json). Long lists keep stride 32.
   g.stride = kGuessStride;
-  while (k < DR_GUESS_LONG_K && g.stride < 128 && n_items / (2 * g.stride) >= 65536) g.stride *= 2;
+  while (k < kGuessLongK && g.stride < 128 && n_items / (2 * g.stride) >= 65536) g.stride *= 2;
   if (const int st = knob_int(DR_KNOB_GUESS_STRIDE, 0); st > 1) g.stride = st;  // A/B knob
   // a whole number of 32-row tiles: the sample is stored tile-transposed
   // (sample_rows_kernel), and rows left out only lower the sample's order
   // statistics, so the guess stays a lower bound
   g.S = n_items / g.stride / kTileItems * kTileItems;
   const double mu = (double)k * (double)g.S / (double)n_items;
-  int ks = (int)ceil(mu + DR_GUESS_SIGMA * sqrt(mu) + 3.0);
+  int ks = (int)ceil(mu + kGuessSigma * sqrt(mu) + 3.0);
   g.ks = ks < k ? ks : k;
-  int ks1 = poisson_tail_rank(mu, DR_GUESS_TAIL);
+  int ks1 = poisson_tail_rank(mu, kGuessTail);
   double z1 = 3.0, c1 = 1.0;
   const bool zk = dr::plan_knob(DR_KNOB_GUESS_Z1, &z1);  // A/B knobs: the round-3 form
   const bool ck = dr::plan_knob(DR_KNOB_GUESS_C1, &c1);
@@ -773,7 +751,7 @@ struct Layout {
 
 Layout make_layout(int64_t n_users, int64_t n_items, int w, int k) {
   Layout L{};
-  L.main = make_plan(n_users, n_items, w, k, DR_GUESS && n_items >= kGuessMinItems);
+  L.main = make_plan(n_users, n_items, w, k, kGuess && n_items >= kGuessMinItems);
   L.g = guess_for(n_items, k, L.main.tail_chunks > 1);
   L.cand = L.main.cand_bytes;
   L.cnt = L.main.cnt_bytes;
@@ -1085,7 +1063,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   as.head_keep = ps.head_keep;
   as.slack = ps.slack;
   as.gap = ps.gap;
-  as.gmax = L.dense ? 2 : DR_SAMPLE_GMAX;
+  as.gmax = L.dense ? 2 : kSampleGmax;
   as.tmax = (float*)ws;  // the candidate region
   as.tmax_tiles = L.g.S / kTileItems;
   DR_SCAN_OR_FAIL(ps, as, false)

@@ -245,3 +245,28 @@ def test_global_threshold_helpers():
     t = threshold_below(s)
     assert bool((t[:3] < s[:3]).all()) and bool((t[5:] < s[5:]).all())
     assert torch.isinf(t[3]) and t[3] < 0 and torch.isinf(t[4]) and t[4] < 0
+
+
+def test_fp64_gap_check_rule_on_cpu():
+    """bench.fp64_gap_check (the bench line's "check" field) on the CPU: exact
+    float64 top-k lists pass; a list missing a clearly-inside item, a score
+    off by more than tol, or an item far below the k-th fail."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    g = torch.Generator().manual_seed(5)
+    nu, ni, d, k = 64, 5000, 32, 10
+    U = (torch.randn(nu, d, generator=g) / d ** 0.5).to(torch.bfloat16)
+    I = (torch.randn(ni, d, generator=g) / d ** 0.5).to(torch.bfloat16)
+    S = U.double() @ I.double().T
+    s, i = torch.topk(S, k, dim=1)
+    sel = torch.arange(nu)
+    ok = bench.fp64_gap_check(U, I, s.float(), i.int(), sel, k, chunk=1000, extra=8)
+    assert ok["ok"] and ok["users_not_in_exact_float64_order"] == 0
+    bad = i.clone()
+    bad[3, 0] = torch.argsort(S[3])[0]  # the user's worst item instead of its best
+    assert not bench.fp64_gap_check(U, I, s.float(), bad.int(), sel, k, chunk=1000, extra=8)["ok"]
+    off = s.float().clone()
+    off[7, 4] += 1e-3
+    assert not bench.fp64_gap_check(U, I, off, i.int(), sel, k, chunk=1000, extra=8)["ok"]

@@ -376,3 +376,93 @@ def test_config5_plan_1m_x_10m_k1000_then_mmr():
     from test_hip_kernels import _mmr_check_positions
 
     assert _mmr_check_positions(remap(picks[sel]), remap(cand), sc, E, 0.5, tol=1e-4) == 0
+
+
+def test_bench_headline_own_tables_fp64():
+    """The call bench.py times, on bench.py's own tables (N(0, 1/sqrt(d))
+    bf16, seeded per 1M-row block; bench.gen_table), checked against float64
+    with the gap-aware rule of test_score_topk_float_tolerance for ~1024
+    users drawn from head, split-tail and last user blocks
+    (bench.check_user_sample / bench.fp64_gap_check): every returned score
+    within tol = 1e-5 sqrt(d/64) of its float64 value, the list sorted within
+    tol, every item above the exact k-th score - 2 tol, and every item clearly
+    inside the exact top-k (margin > 2 tol) returned. The integer-table plan
+    tests above fix the same plan with exact scores; this one is the timed
+    workload's own survivor and compaction dynamics."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    U_n, I_n, d, k = 1_000_000, 10_000_000, 128, 100
+    U = bench.gen_table(U_n, d, 1, DEV)
+    I = bench.gen_table(I_n, d, 2, DEV)
+    plan = ops.score_topk_plan(U_n, I_n, torch.bfloat16, d, k)
+    assert plan["tail_chunks"] > 1 and plan["sample_stride"] == 128  # the headline's plan
+    s, i = ops.score_topk(U, I, k)
+    sel = bench.check_user_sample(U_n, I_n, d, k, 1024)
+    upw, head = plan["users_per_wg"], plan["head_blocks"]
+    assert (sel < head * upw).sum() > 300 and (sel >= (plan["user_blocks"] - 1) * upw).sum() > 200
+    res = bench.fp64_gap_check(U, I, s, i, sel, k)
+    assert res["ok"], res
+    assert res["users_checked"] >= 1000
+
+
+def test_bpr_config3_full_size():
+    """Config 3 at its BASELINE size: one
+    pair_wise_train_loop-equivalent step (divrec/train/utils.py:144-152 with
+    LogSigmoidDifferenceLoss, log_sigmoid_difference_loss.py:11-14) on two
+    1M x 128 fp32 tables with 1,048,576 uniform triples, through the fused
+    dr_bpr_fwd_bwd, against float64 on the device: the mean loss within rel
+    1e-6; every AUC hit equal to (s_p >= s_n) except on float64 near-ties
+    (|s_p - s_n| <= 1e-5), where fp32 summation order may flip it; both dense
+    gradient tables (fp32 atomics, any order) within rel 1e-4 of float64
+    index_add_ (the tolerance of test_bpr_fwd_bwd) everywhere; then one
+    dr_adam_dense step equal to torch.optim.Adam on 4096 sampled rows of each
+    table (atol 1e-6, the test_adam_dense_matches_torch bar)."""
+    g = torch.Generator(device=DEV).manual_seed(33)
+    n, d, B = 1_000_000, 128, 1 << 20
+    U = torch.randn(n, d, generator=g, device=DEV) / d ** 0.5
+    I = torch.randn(n, d, generator=g, device=DEV) / d ** 0.5
+    uid = torch.randint(0, n, (B,), generator=g, device=DEV)
+    pid = torch.randint(0, n, (B,), generator=g, device=DEV)
+    nid = torch.randint(0, n, (B,), generator=g, device=DEV)
+    gU = torch.zeros_like(U)
+    gI = torch.zeros_like(I)
+    loss, hit = ops.bpr_fwd_bwd(U, I, uid, pid, nid, 1.0 / B, gU, gI)
+
+    Ud, Id = U.double(), I.double()
+    u, p, q = Ud[uid], Id[pid], Id[nid]
+    sp, sn = (u * p).sum(1), (u * q).sum(1)
+    x = sp - sn
+    ref_loss = torch.nn.functional.softplus(-x).mean()
+    assert abs(loss.double().mean() - ref_loss) <= 1e-6 * abs(ref_loss)
+    flip = (hit.bool() != (sp >= sn))
+    assert not bool((flip & (x.abs() > 1e-5)).any())
+    gcoef = (-torch.sigmoid(-x) / B).unsqueeze(1)
+    # a user row's term g (p - n) may be formed as g p - g n in fp32: its
+    # error scales with |g| (|p| + |n|), not with the (cancelling) difference
+    tU, mU, tI = gcoef * (p - q), gcoef.abs() * (p.abs() + q.abs()), gcoef * u
+    del p, q, u
+    for got, idx, terms, mags in ((gU, (uid,), (tU,), (mU,)),
+                                  (gI, (pid, nid), (tI, -tI), (tI.abs(), tI.abs()))):
+        ref = torch.zeros_like(Ud)
+        mag = torch.zeros_like(Ud)  # sum of |terms|: the scale of an fp32 sum's error
+        for ix, t, a in zip(idx, terms, mags):
+            ref.index_add_(0, ix, t)
+            mag.index_add_(0, ix, a)
+        err = (got.double() - ref).abs()
+        # rel 1e-4 of the value, or 1e-5 of the terms' magnitude where the
+        # terms cancel (a row's few fp32 adds in any order)
+        assert bool((err <= torch.maximum(1e-4 * ref.abs(), 1e-5 * mag)).all()), float(err.max())
+        del ref, mag, err
+    del tU, mU, tI
+
+    rows = torch.randperm(n, generator=g, device=DEV)[:4096]
+    for P, G in ((U, gU), (I, gI)):
+        ref = P[rows].clone().requires_grad_(True)
+        ref.grad = G[rows].clone()
+        opt = torch.optim.Adam([ref], lr=1e-3)
+        opt.step()
+        m, v = torch.zeros_like(P), torch.zeros_like(P)
+        ops.adam_dense(P, G, m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1)
+        assert torch.allclose(P[rows], ref.detach(), atol=1e-6, rtol=0)

@@ -1,13 +1,9 @@
 #!/bin/bash
-# Build the A/B variants of the score-scan kernel timed by tools/variant_bench.py
-# (one library per variant, same sources, different -D knobs).
+# Build the A/B variant of the score scan that the product keeps a knob for
+# (one library per variant, same sources, a different -D): the d = 128 stage
+# size, 64 KB against the product's 72 KB (profiles/r06/stage_fetch/: time
+# and PMC FETCH side by side). Planner choices are runtime knobs instead
+# (dr_set_plan_knob; tools/variant_bench.py tags "product@knob=value").
 set -e
 B="python diversity-recommendations_amd/build_native.py --jobs 8"
-$B --variant base -D DR_NUT=2 -D DR_STAGE_BYTES=16384 -D DR_RING=4 -D DR_PRIO=0 -D DR_APIPE=0 -D DR_FLUSH_GAP=100000 -D DR_PREPASS=0
-$B --variant nut2 -D DR_NUT=2
-$B --variant prio -D DR_PRIO=1
-$B --variant noapipe -D DR_APIPE=0
-$B --variant pre -D DR_PREPASS=1
-$B --variant ring3 -D DR_RING=3
-$B --variant gap32 -D DR_FLUSH_GAP=32
-$B --variant gap256 -D DR_FLUSH_GAP=256
+$B --variant stage64 -D DR_STAGE_BYTES_WIDE=65536
