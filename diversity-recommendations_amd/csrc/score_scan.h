@@ -85,9 +85,6 @@ constexpr int kStageBlocks = 64;  // staged lane blocks per wave (>= 64: one use
 constexpr int kWavesScan = 8;
 constexpr int waves_for(int) { return kWavesScan; }
 constexpr int kMaxWaves = kWavesScan;
-// Longest catalog a staged (W <= 64) scan takes: its staged blocks name their
-// tile in 23 bits (dr_score_topk refuses longer ones).
-constexpr int64_t kMaxStagedRows = (int64_t)32 << 23;
 constexpr int kTileItems = 32;
 constexpr int kSlack = 32;  // keys kept beyond k by a compaction
 constexpr int kFlushGap = kFlushGapDefault;
@@ -697,9 +694,11 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
   uint32_t* ucnt = reinterpret_cast<uint32_t*>(wbase);
   uint32_t* hist = reinterpret_cast<uint32_t*>(wbase + UPW * 4);
   float* blk_val = reinterpret_cast<float*>(wbase + UPW * 4);  // [SB][16], 16-B aligned
-  // [SB] {tile of the unit | slot << 23 | h << 31, threshold bits}: one
-  // ds_write_b64 per staged lane; 23 tile bits cover kMaxStagedRows (the host
-  // refuses longer catalogs at the staged widths)
+  // [SB] {tile within the stage | slot << 8 | h << 16, threshold bits}: one
+  // ds_write_b64 per staged lane. A stage's blocks are always resolved before
+  // the next stage begins (stage end, or an overflow inside the stage), so
+  // the tile is named relative to the stage's first tile (stage_t0; SR <= 255
+  // tiles): no bound on the catalog length
   uint2* blk_meta = reinterpret_cast<uint2*>(blk_val + SB * 16);
   const uint32_t lds_ring = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
   // This lane's A-fragment byte offset for k-step s in a tile is
@@ -784,6 +783,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
     // inside the loop, draining the ring).
     wait_vmcnt<0>();
     for (int s = lane; s < UPW; s += 64) ucnt[s] = 0;
+    int stage_t0 = 0;   // first tile of the stage being scanned (staged blocks are relative to it)
     int vmc = 0;        // VMEM instructions issued by this wave in this unit
     int vm_done = 0;    // every op issued before this count has completed
     int vs[kRing - 1];  // vmc right after each outstanding stage's DMA
@@ -942,6 +942,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
     // into the slot of stage s-1, which every wave finished reading.
     auto boundary = [&](int st) {
       DG_T0(t_b);
+      stage_t0 = st * SR;
       if (vs[0] > vm_done) wait_vmcnt_dyn(vmc - vs[0]);
       __builtin_amdgcn_s_barrier();
 #pragma unroll
@@ -971,6 +972,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
     // parallel across blocks, off the MFMA loop. A block's threshold is the one
     // at staging time: thresholds only rise, so it admits a superset.
     int nblk = 0;  // staged blocks (wave-uniform)
+    static_assert(SR <= 255, "stage-relative tile field is 8 bits");
     // BATCHED: the stage-end form (accumulators dead there); the in-loop
     // overflow call keeps the light per-score form, whose few registers fit
     // beside the live accumulators
@@ -983,9 +985,9 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
         const bool live = i < nblk;
         const int ii = live ? i : 0;
         const uint2 meta = blk_meta[ii];
-        const uint32_t tl = meta.x & 0x7fffffu;  // tile of the unit
-        const uint32_t slot = (meta.x >> 23) & 0xffu;
-        const int hh = (int)(meta.x >> 31);
+        const uint32_t tl = (uint32_t)stage_t0 + (meta.x & 0xffu);  // tile of the unit
+        const uint32_t slot = (meta.x >> 8) & 0xffu;
+        const int hh = (int)((meta.x >> 16) & 1u);
         const float th = __uint_as_float(meta.y);
         const int64_t row0 = i_beg + (int64_t)tl * kTileItems;
         const uint32_t gb = (uint32_t)(a.item_base + row0);
@@ -1085,8 +1087,8 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
           for (int q = 0; q < 4; ++q)
             dst[q] = make_float4(acc[ut][4 * q], acc[ut][4 * q + 1], acc[ut][4 * q + 2],
                                  acc[ut][4 * q + 3]);
-          blk_meta[i] = make_uint2((uint32_t)t | ((uint32_t)((g0 + ut) * 32 + col) << 23) |
-                                       ((uint32_t)h << 31),
+          blk_meta[i] = make_uint2((uint32_t)(t - stage_t0) | ((uint32_t)((g0 + ut) * 32 + col) << 8) |
+                                       ((uint32_t)h << 16),
                                    __float_as_uint(thr[g0 + ut]));
         }
         nblk += n;
@@ -1239,7 +1241,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
         float4* dst = reinterpret_cast<float4*>(blk_val + i * 16);
 #pragma unroll
         for (int q = 0; q < 4; ++q) dst[q] = make_float4(ac[4 * q], ac[4 * q + 1], ac[4 * q + 2], ac[4 * q + 3]);
-        blk_meta[i] = make_uint2((uint32_t)t | ((uint32_t)(u * 32 + col) << 23) | ((uint32_t)h << 31),
+        blk_meta[i] = make_uint2((uint32_t)(t - stage_t0) | ((uint32_t)(u * 32 + col) << 8) | ((uint32_t)h << 16),
                                  __float_as_uint(thr[u]));
       }
       nblk += n;

@@ -931,8 +931,6 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   DR_CHECK_ARG(cap_for(w, k) > 0, "k too large for this d");
   DR_CHECK_ARG(item_base >= 0 && item_base + n_items < 0x7fffffffLL,
                "global item ids must fit int32");
-  DR_CHECK_ARG(w > 64 || n_items <= kMaxStagedRows,
-               "catalog slices above 2^28 rows need rows wider than 128 bytes");
   DR_CHECK_ARG((excl_rowptr == nullptr) == (excl_items == nullptr),
                "excl_rowptr and excl_items must both be set or both be NULL");
   if (n_users == 0) return DR_OK;
@@ -1208,8 +1206,6 @@ extern "C" int dr_score_topk_seeded(const void* user_table, const int64_t* user_
   DR_CHECK_ARG(cap_for(w, k) > 0, "k too large for this d");
   DR_CHECK_ARG(item_base >= 0 && item_base + n_items < 0x7fffffffLL,
                "global item ids must fit int32");
-  DR_CHECK_ARG(w > 64 || n_items <= kMaxStagedRows,
-               "catalog slices above 2^28 rows need rows wider than 128 bytes");
   DR_CHECK_ARG((excl_rowptr == nullptr) == (excl_items == nullptr),
                "excl_rowptr and excl_items must both be set or both be NULL");
   if (n_users == 0) return DR_OK;

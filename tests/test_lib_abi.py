@@ -260,3 +260,20 @@ def test_distributed_guess_ranks_mirror_the_planner():
             if p["sample_stride"]:
                 assert guess_ranks(k, p["sample_rows"] / n) == (p["first_tier_rank"],
                                                                 p["sample_rank"]), (n, k)
+
+
+def test_staged_scans_take_catalogs_above_2_28_rows():
+    """the staged (d <= 64 bf16, d = 32 fp32) scans used to refuse
+    catalog slices above 2^28 rows (a staged block named its tile in 23 bits).
+    The tile is now named relative to its stage, so the call gets past the
+    argument checks at 2^28 + 32 rows and its workspace and plan exist; the
+    scan itself is exact there (tests/test_real_plans.py)."""
+    lib = _backend.load_library()
+    n = (1 << 28) + 32
+    for dtype, d in ((_backend.DR_BF16, 32), (_backend.DR_BF16, 64), (_backend.DR_F32, 32)):
+        assert lib.dr_score_topk_workspace(64, n, dtype, d, 10) > 0
+        out = (ctypes.c_int64 * 13)()
+        assert lib.dr_score_topk_plan(64, n, dtype, d, 10, out, 13) == 0
+        rc = lib.dr_score_topk(None, None, 64, None, n, 0, dtype, d, 10, None, None, None, None,
+                               None, 0, None)
+        assert rc == -1 and b"null pointer" in lib.dr_last_error()

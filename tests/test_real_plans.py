@@ -466,3 +466,40 @@ def test_bpr_config3_full_size():
         m, v = torch.zeros_like(P), torch.zeros_like(P)
         ops.adam_dense(P, G, m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1)
         assert torch.allclose(P[rows], ref.detach(), atol=1e-6, rtol=0)
+
+
+def test_staged_scan_beyond_2_28_rows_exact():
+    """A d = 32 bf16 (staged) scan of one unit longer than 2^28 rows: 64
+    users over 2^28 + 4096 + 17 integer-valued item rows with the catalog
+    split off (scan_split = 1), so a single workgroup's unit names tiles past
+    2^23 (the old 23-bit staged-block field). A few planted hot rows sit
+    past row 2^28 and near the end. Lists equal the exact top-k from a
+    float64 scan of the same rows (integer tables: exact scores, ties broken
+    by id)."""
+    from divrec import _backend
+    rng = np.random.default_rng(28)
+    nu, ni, d, k = 64, (1 << 28) + 4096 + 17, 32, 10
+    U = torch.from_numpy(rng.integers(-2, 3, size=(nu, d)).astype(np.float32)).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    I = torch.randint(-1, 2, (ni, d), generator=g, device=DEV, dtype=torch.int8).to(torch.bfloat16)
+    hot = torch.tensor([(1 << 28) + 5, (1 << 28) + 4000, ni - 1, 17], device=DEV)
+    I[hot] = (U[:4] * 2).to(torch.bfloat16)  # user j's best possible row for j < 4
+    Ub = U.to(torch.bfloat16)
+    with _backend.plan_knobs(scan_split=1):
+        s, i = ops.score_topk(Ub, I, k)
+    best_s = torch.full((nu, k), -float("inf"), dtype=torch.float64, device=DEV)
+    best_i = torch.zeros((nu, k), dtype=torch.int64, device=DEV)
+    Ud = U.double()
+    for c0 in range(0, ni, 1 << 24):
+        S = Ud @ I[c0:c0 + (1 << 24)].double().T
+        # ties by id ascending: the key (score, -id), scores integral
+        key = S * (1 << 30) - torch.arange(c0, c0 + S.shape[1], device=DEV, dtype=torch.float64)
+        kv, ki = torch.topk(key, k, dim=1)
+        cand_i = torch.cat([best_i, ki + c0], 1)
+        cand_k = torch.cat([best_s * (1 << 30) - best_i.double(), kv], 1)
+        top = torch.topk(cand_k, k, dim=1).indices
+        best_i = torch.gather(cand_i, 1, top)
+        best_s = (Ud.unsqueeze(1) * I[best_i].double()).sum(-1)
+    assert torch.equal(i.long(), best_i)
+    assert torch.equal(s.double(), best_s)
+    assert bool((i[:4, 0].long() == hot).all())
