@@ -170,9 +170,12 @@ def cpu_baseline(U: torch.Tensor, I: torch.Tensor, recs: torch.Tensor, k: int, b
         "sample": f"oracle.reference_loop_topk (the reference get_model_recommendations loop "
                   f"restated in torch: frozenset difference, LongTensor, torch.full, embedding "
                   f"gather + sum(u*i), argsort, slice, tolist) for {n_users} users x {n_items} "
-                  f"items in {dt:.1f}s on {threads} threads; ILD: oracle.ild_embedding_f64 on "
-                  f"{len(rh)} users -> {len(rh) / ild_dt:.0f} users/s (1 thread)",
+                  f"items in {dt:.1f}s on {threads} threads; ILD: oracle.ild_embedding_f64, the "
+                  f"VECTORISED float64 form (one Gram matrix per list), not the reference's "
+                  f"itertools.combinations loop (~43 users/s at k = 100), on "
+                  f"{len(rh)} users -> {len(rh) / ild_dt:.0f} users/s",
         "ild_users_per_s": len(rh) / ild_dt,
+        "ild_kind": "vectorised float64 (oracle.ild_embedding_f64), not the reference's pair loop",
         "vectorized": {"value": n_vec * n_items / vec_dt, "unit": "scored pairs/s",
                        "cores": torch.get_num_threads(),
                        "sample": f"torch fp32 ({n_vec} x {Ih.shape[1]}) @ ({Ih.shape[1]} x {n_items}) "

@@ -64,10 +64,12 @@ enum {
 // (rounds 2 and 5), 12 / 16 waves at d <= 64, SIMD-pair priorities, two
 // accumulator sets in ping-pong, the A fragments read per half chain, other
 // stage sizes, slacks and flush gaps. The one -D knob kept is the d = 128
-// stage size (DR_STAGE_BYTES_WIDE: its L2-reuse / time trade-off is
-// re-measured with PMC FETCH beside the time, profiles/r06/stage_fetch/).
+// stage size (DR_STAGE_BYTES_WIDE, tools/build_variants.sh), re-measured in
+// round 6 with PMC FETCH beside the time at the headline (1M x 10M, k = 100;
+// profiles/r06/stage_fetch/): 72 KB 1770 ms, main-scan FETCH 227.6 GB;
+// 64 KB 1776 ms, 243.0 GB. 72 KB wins both.
 #ifndef DR_STAGE_BYTES_WIDE
-#define DR_STAGE_BYTES_WIDE 73728  // ring slot for d = 128 (9 tiles: 72 KB; 64 KB measured +0.4-0.8 %)
+#define DR_STAGE_BYTES_WIDE 73728  // ring slot for d = 128 (9 tiles: 72 KB)
 #endif
 constexpr int kStageBytesOther = 32768;  // ring slot for d = 256 / 512 (three slots)
 constexpr int kRingOther = 3;
@@ -76,8 +78,8 @@ constexpr int kNutWide = 4;           // user tiles of 32 per wave for d = 128
 constexpr int kNutNarrow = 8;         // for d <= 64 (+14 % at d = 64, 1M x 1M, against 4)
 constexpr int kFlushGapDefault = 96;  // new keys a buffer takes past k + kSlack before compaction
 // Survivors are staged in LDS and resolved per stage for d <= 64 (twice as
-// dense per MFMA there: 4 % faster), stored directly for d >= 128 (4 %
-// faster there).
+// dense per MFMA there: 4 % faster) and for d = 128 long lists (below),
+// stored directly for other d >= 128 (4 % faster there at k = 100).
 constexpr int kStageBlocks = 64;  // staged lane blocks per wave (>= 64: one user tile always fits)
 
 // Waves per workgroup of a scan (one workgroup per CU): two per SIMD, 256
@@ -101,17 +103,25 @@ constexpr int kFlushGap = kFlushGapDefault;
 // -1.7 % at config 2, -0.25 % at d = 32; the stage margin of 448 keys puts
 // k = 100 on CAP 1024 there). d = 256 spills with 64-KB stages.
 constexpr int kStageBytesNarrow = 57344;  // ring slot for d <= 64
-constexpr int stage_bytes_for(int w) {
-  return w == 128 ? DR_STAGE_BYTES_WIDE : (w <= 64 ? kStageBytesNarrow : kStageBytesOther);
+// Long lists at d = 128 (CAP 2048, k > ~670): survivors are dense enough
+// (k = 1000: direct stores were 16 % of wave time) that the d <= 64 staging
+// pays there too (round 6: 2046 -> 2009 ms at 1M x 10M, k = 1000, lists
+// identical, profiles/r06/long_staged/); its LDS area (8 waves x 4.6 KB) fits
+// beside two 56-KB slots (7 tiles) instead of 72-KB ones.
+constexpr bool long_staged(int w, int cap) { return w == 128 && cap == 2048; }
+constexpr int kStageBytesLong = 57344;
+constexpr int stage_bytes_for(int w, int cap) {
+  return long_staged(w, cap) ? kStageBytesLong
+       : w == 128 ? DR_STAGE_BYTES_WIDE : (w <= 64 ? kStageBytesNarrow : kStageBytesOther);
 }
 constexpr int kRingNarrow = 2;  // ring slots for d <= 64
 constexpr int ring_for(int w) { return w == 128 ? kRingWide : (w <= 64 ? kRingNarrow : kRingOther); }
 
-template <int D>  // D = W, the row's width in bf16 units (row bytes / 2)
+template <int D, int CAP>  // D = W, the row's width in bf16 units (row bytes / 2)
 struct TileGeom {
   static constexpr int WAVES = waves_for(D);
   static constexpr int THREADS = WAVES * 64;
-  static constexpr int STAGE_BYTES = stage_bytes_for(D);  // one LDS ring slot
+  static constexpr int STAGE_BYTES = stage_bytes_for(D, CAP);  // one LDS ring slot
   static constexpr int RING = ring_for(D);                // slots (RING - 1 stages in flight)
   static constexpr int LPT = STAGE_BYTES / 16 / THREADS;  // LDS-DMA per thread per stage
   static constexpr int KSTEPS = D / 16;                 // MFMA k-steps per row
@@ -219,10 +229,10 @@ __device__ __forceinline__ int64_t uni64(int64_t v) {
 // opaque, so hipcc cannot hoist 64-bit per-lane addresses out of the tile loop
 // (they cost registers the loop does not have, and their spill reloads wait
 // vmcnt(0), draining the ring).
-template <int D>
+template <int D, int CAP>
 __device__ __forceinline__ void issue_stage(const char* __restrict__ I, int64_t n_items,
                                             int64_t row0, uint32_t lds_stage) {
-  using G = TileGeom<D>;
+  using G = TileGeom<D, CAP>;
   constexpr int ROWS = G::SR * kTileItems;
   uint32_t tid = threadIdx.x;
   asm volatile("" : "+v"(tid));
@@ -647,7 +657,7 @@ template <int W, int CAP, bool SEEDED, bool F32, bool GMAX = false>
 __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_scan_kernel(TopkArgs a) {
   static_assert(!(GMAX && SEEDED), "tile-max scans are the (unseeded) sample scans");
   constexpr int D = W;  // geometry is by row bytes: an fp32 row of d is a bf16 row of 2d
-  using G = TileGeom<D>;
+  using G = TileGeom<D, CAP>;
   constexpr int NU_T = nut_for(D);
   constexpr int NG = ngroup_for(D);  // user tiles per accumulator group
   constexpr int NGRP = NU_T / NG;    // groups scored against each item tile
@@ -664,7 +674,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
   constexpr int RING_BYTES = kRing * kStageBytes;
   // per wave: per-user key counts, radix histogram, staged survivor blocks
   // (16 scores + one 8-B record: tile | slot | h, threshold)
-  constexpr bool STAGED = D <= 64;
+  constexpr bool STAGED = D <= 64 || long_staged(D, CAP);
   constexpr int SB = STAGED ? kStageBlocks : 0;
   // stage_hits resolves a full stage area, then stages up to 64 lanes of one
   // user tile: the area must hold a whole wave's worth of blocks
@@ -948,7 +958,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
 #pragma unroll
       for (int i = 0; i + 1 < kRing - 1; ++i) vs[i] = vs[i + 1];
       if (st + kRing - 1 < nst) {
-        issue_stage<D>(a.I, a.n_items, i_beg + (int64_t)(st + kRing - 1) * SR * kTileItems,
+        issue_stage<D, CAP>(a.I, a.n_items, i_beg + (int64_t)(st + kRing - 1) * SR * kTileItems,
                        lds_ring + ((st + kRing - 1) % kRing) * kStageBytes);
         vmc += kLpt;
       }
@@ -957,7 +967,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
       DG_CNT(kDgNStages);
     };
     for (int st = 0; st < kRing - 1 && st < nst; ++st) {
-      issue_stage<D>(a.I, a.n_items, i_beg + (int64_t)st * SR * kTileItems,
+      issue_stage<D, CAP>(a.I, a.n_items, i_beg + (int64_t)st * SR * kTileItems,
                      lds_ring + st * kStageBytes);
       vmc += kLpt;
 #pragma unroll

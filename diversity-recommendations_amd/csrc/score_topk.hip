@@ -474,16 +474,15 @@ int device_cus() {
   return cus > 0 ? cus : 256;
 }
 
-int64_t stage_items_for(int w) {
-  return (int64_t)(stage_bytes_for(w) / (kTileItems * w * 2)) * kTileItems;
+int64_t stage_items_for(int w, int cap) {
+  return (int64_t)(stage_bytes_for(w, cap) / (kTileItems * w * 2)) * kTileItems;
 }
 
 // Smallest candidate capacity that leaves at least 32 keys of headroom above
 // k + kSlack once a stage's worth of new keys (the margin) is reserved.
 int cap_for(int w, int k) {
-  const int margin = (int)stage_items_for(w);
   for (int cap = 512; cap <= 2048; cap <<= 1)
-    if (k + kSlack + 32 <= cap - margin) return cap;
+    if (k + kSlack + 32 <= cap - (int)stage_items_for(w, cap)) return cap;
   return -1;
 }
 
@@ -527,7 +526,7 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   p.n_ublocks = dr::ceil_div(n_users, p.users_per_wg);
   p.n_users_pad = p.n_ublocks * p.users_per_wg;
   const int64_t slots = device_cus();
-  const int64_t stage_items = stage_items_for(w);
+  const int64_t stage_items = stage_items_for(w, p.cap);
   int max_c_override = 0;
   const int64_t B = p.n_ublocks;
   const int64_t H = (B / slots) * slots;
@@ -595,7 +594,7 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
 // (the sort instances start at 256 keys).
 int flush_keys(const Plan& p, int w, int k) {
   const int f = k + p.slack + p.gap;
-  const int m = p.cap - (int)stage_items_for(w);
+  const int m = p.cap - (int)stage_items_for(w, p.cap);
   return f < m ? f : m;
 }
 int head_keys(const Plan& p, int w, int k) {
@@ -1128,7 +1127,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
     dsa.max_c = kMaxRescanChunks;
     dsa.buf_blocks = a2.buf_blocks;
     dsa.n_items = n_items;
-    dsa.stage_items = stage_items_for(w);
+    dsa.stage_items = stage_items_for(w, p.cap);
     hipLaunchKernelGGL(topk_finalize_stream_kernel, dim3((unsigned)dr::ceil_div(n_users, 4)),
                        dim3(256), 0, s, a.cand, a.cnt, dsa, p.cap, n_users, k, excl_rowptr,
                        excl_items, out_scores, out_items, fpos, fcnt, frows, fcnt + 1, frows2,

@@ -30,9 +30,14 @@ from .base_losses import DatasetAwareLoss, RecommendationsAwareLoss
 class EmbeddingDistance:
     """Lazy D from item embeddings (computed per pair inside the kernel).
 
-    The kernel reads a bf16 table; a float table is rounded to bf16 once, and
-    a width without a kernel instance (e.g. the reference experiments' 100) is
-    zero-padded once."""
+    The kernel reads a bf16 table; a float table is rounded to bf16, and a
+    width without a kernel instance (e.g. the reference experiments' 100) is
+    zero-padded. That device copy is kept between calls and rebuilt whenever
+    the source table changes in a way torch records: another tensor assigned
+    to ``item_table``, a new storage (data_ptr), shape or device, or an
+    in-place update through autograd-visible ops (its ``_version``, e.g. an
+    optimizer step). Writes torch cannot see (``.data`` views of another
+    tensor, raw pointers, a kernel writing the storage) need ``refresh()``."""
 
     KINDS = ("cosine", "dot", "euclidean")
 
@@ -42,15 +47,25 @@ class EmbeddingDistance:
         self.kind = kind
         self.item_table = item_table
         self._dev_table = None
+        self._key = None
+
+    def refresh(self) -> None:
+        """Drop the device copy: the next call rebuilds it from item_table."""
+        self._dev_table = None
+        self._key = None
+
+    def _source_key(self, device: torch.device):
+        t = self.item_table
+        return (str(device), t.data_ptr(), tuple(t.shape), t.dtype, t.device, t._version)
 
     def table(self, device: torch.device) -> torch.Tensor:
-        t = self._dev_table
-        if t is None or t.device != device:
+        key = self._source_key(device)
+        if self._dev_table is None or key != self._key:
             t = self.item_table.detach().to(device=device, dtype=torch.bfloat16).contiguous()
             # widths without a kernel instance: zero columns change no distance
             t = ops.pad_columns(t, ops._width_of(ops.ILD_WIDTHS, t.size(1), "embedding ILD"))
-            self._dev_table = t
-        return t
+            self._dev_table, self._key = t, key
+        return self._dev_table
 
 
 class LabelEquality:

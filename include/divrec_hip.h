@@ -139,7 +139,15 @@ int dr_gather_dot_backward(const float* user_table, int64_t n_user_rows, const f
  *     slots with no candidate hold item -1 and score -inf.
  *   workspace of dr_score_topk_workspace(...) bytes (query with identical args,
  *     with the device that runs the call current: the launch plan, and with it
- *     the size, depends on the device's CU count).
+ *     the size, depends on the device's CU count). Its size: candidate buffers
+ *     of n_users (rounded up to a user block) x CAP x 8 B (CAP 512, 1024 or
+ *     2048 by d and k), plus rows for the extra chunks of a split tail; for
+ *     catalogs of 2^18 rows or more (the guessed thresholds) that region is
+ *     instead the sample scan's dense [users x sample tiles] fp32 tile-max
+ *     matrix when that is larger and within the SAMPLE_DENSE budget (16 GiB by
+ *     default; 1M x 10M at d = 128: 9.8 GB against 8.5 GB of buffers), plus
+ *     about 40 B per user of thresholds and fail lists and a copy of the
+ *     sample rows.
  */
 size_t dr_score_topk_workspace(int64_t n_users, int64_t n_items, int dtype, int d, int k);
 int dr_score_topk(const void* user_table, const int64_t* user_ids, int64_t n_users,

@@ -270,3 +270,30 @@ def test_fp64_gap_check_rule_on_cpu():
     off = s.float().clone()
     off[7, 4] += 1e-3
     assert not bench.fp64_gap_check(U, I, off, i.int(), sel, k, chunk=1000, extra=8)["ok"]
+
+
+def test_embedding_distance_device_copy_follows_its_table():
+    """EmbeddingDistance keeps its bf16, zero-padded copy between calls and
+    rebuilds it when the source changes in a way torch records (in-place
+    update, new tensor, new shape) or on refresh() (no stale
+    padded copy). Host logic only: the copy is built on the CPU here."""
+    import torch
+    from divrec.losses import EmbeddingDistance
+
+    cpu = torch.device("cpu")
+    E = torch.randn(10, 100)
+    D = EmbeddingDistance(E, "cosine")
+    t0 = D.table(cpu)
+    assert t0.shape == (10, 128) and t0.dtype == torch.bfloat16 and not t0[:, 100:].any()
+    assert D.table(cpu) is t0  # cached
+    E.add_(1.0)  # an optimizer-style in-place step bumps the version
+    t1 = D.table(cpu)
+    assert t1 is not t0 and torch.equal(t1[:, :100], E.to(torch.bfloat16))
+    D.item_table = torch.randn(12, 100)
+    assert D.table(cpu).shape == (12, 128)
+    t2 = D.table(cpu)
+    D.item_table.data[0, 0] = 5.0  # a .data write: no version torch records
+    assert D.table(cpu) is t2  # documented: such writes need refresh()
+    D.refresh()
+    t3 = D.table(cpu)
+    assert t3 is not t2 and float(t3[0, 0]) == 5.0
