@@ -536,6 +536,7 @@ __device__ uint64_t g_ild_diag[8192][8];
 #define ILD_ADD(slot, t0) ((void)0)
 #endif
 constexpr int kStreamWaves = 4;
+constexpr int kStreamMinK = 40;  // shorter lists take the one-wave-per-user kernel
 constexpr int kStreamMaxBufs = 16;
 constexpr int kStreamLds = 163840;
 constexpr int kStreamHead = kStreamWaves * (128 * 4 + kStreamMaxBufs * 4);  // per-row terms, bad flags
@@ -882,9 +883,12 @@ int launch_embedding(const R* recs, int64_t n_users, int k, const __bf16* E, int
     }
   }
   // the whole list fits in registers for d <= 128 (k <= 128 = 4 tiles):
-  // streamed by default, one wave per user with DR_KNOB_ILD_STREAM = 0 (A/B)
+  // streamed for k > kStreamMinK, one wave per user below (short lists: the
+  // stream's per-user pipeline overhead dominates; d = 128, 1M users:
+  // k = 10 0.72 against 1.2 ms, k = 40 2.41 against 2.44, k = 64 3.04
+  // against 2.86, profiles/r06/ild_ab/); DR_KNOB_ILD_STREAM forces either
   double sv;
-  const bool stream = !(dr::plan_knob(DR_KNOB_ILD_STREAM, &sv) && sv == 0.0);
+  const bool stream = dr::plan_knob(DR_KNOB_ILD_STREAM, &sv) ? sv != 0.0 : k > kStreamMinK;
   if (stream && (d == 32 || d == 64 || d == 128)) {
     if (d == 32) launch_stream<R, 32>(recs, n_users, k, E, ni, kind, out, err, s);
     else if (d == 64) launch_stream<R, 64>(recs, n_users, k, E, ni, kind, out, err, s);

@@ -720,7 +720,8 @@ def test_ild_embedding(d, k, kind):
 @pytest.mark.parametrize("k", [1, 2, 10, 31, 33, 64, 100, 128])
 @pytest.mark.parametrize("rec_dtype", [torch.int64, torch.int32])
 def test_ild_embedding_stream_matches_wave_per_user(d, k, rec_dtype):
-    """The streamed persistent-grid ILD (k <= 128, d <= 128; the default):
+    """The streamed persistent-grid ILD (k <= 128, d <= 128; the default for
+    k > 40, forced here by ild_stream = 1 for every k):
     int64 and int32 lists, more users than the grid's waves (each wave's
     pipeline runs many users, its last ones re-issued as padding), a ring of
     one list's pieces, of 1.5 and 3 lists (ild_bufs) and the LDS-sized
@@ -744,7 +745,7 @@ def test_ild_embedding_stream_matches_wave_per_user(d, k, rec_dtype):
         ni = -(-k // (64 // (d // 8)))  # 1-KB pieces per list
         for bufs in (None, ni, max(ni * 3 // 2, ni + 1), min(3 * ni, 64)):
             err = torch.zeros(1, dtype=torch.int32, device=DEV)
-            with _backend.plan_knobs(**({} if bufs is None else {"ild_bufs": bufs})):
+            with _backend.plan_knobs(ild_stream=1, **({} if bufs is None else {"ild_bufs": bufs})):
                 out = torch.empty(nu, dtype=torch.float32, device=DEV)
                 rc = _backend.lib().dr_ild_embedding(
                     rt.data_ptr(), _backend.dtype_code(rec_dtype), nu, k, Et.data_ptr(), 5000, d,
@@ -768,6 +769,20 @@ def test_ild_embedding_stream_matches_wave_per_user(d, k, rec_dtype):
             assert np.allclose(got[ok][:300], ref, rtol=2e-5, atol=2e-5 * np.abs(ref).max())
 
 
+def test_ild_embedding_routes_short_lists_to_the_per_user_kernel():
+    """Default plan: lists of k <= 40 take the one-wave-per-user kernel (faster
+    there), longer ones the streamed kernel: the default output equals the
+    forced kernel's bit for bit on each side of the bound."""
+    rng = np.random.default_rng(40)
+    E = _bf16(oracle.as_bf16_f32(rng.standard_normal((3000, 128)).astype(np.float32)))
+    for k, forced in ((10, 0), (40, 0), (41, 1), (64, 1)):
+        rt = torch.from_numpy(rng.integers(0, 3000, size=(2000, k))).to(DEV)
+        got = ops.ild_embedding(rt, E, "cosine")
+        with _backend.plan_knobs(ild_stream=forced):
+            ref = ops.ild_embedding(rt, E, "cosine")
+        assert torch.equal(got, ref), k
+
+
 def test_ild_embedding_stream_small_grids():
     """Fewer users than waves (idle waves return at once), one user, and a
     wave with exactly one user: the pipeline's padding re-issues that user."""
@@ -776,7 +791,7 @@ def test_ild_embedding_stream_small_grids():
     for nu in (1, 3, 1023, 1025):
         recs = rng.integers(0, 700, size=(nu, 100))
         rt = torch.from_numpy(recs).to(DEV)
-        got = ops.ild_embedding(rt, _bf16(E), "cosine").cpu().numpy()
+        got = ops.ild_embedding(rt, _bf16(E), "cosine").cpu().numpy()  # k = 100: streamed
         with _backend.plan_knobs(ild_stream=0):
             base = ops.ild_embedding(rt, _bf16(E), "cosine").cpu().numpy()
         assert np.allclose(got, base, rtol=2e-5, atol=1e-6)

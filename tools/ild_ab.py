@@ -60,13 +60,29 @@ def main():
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--kind", default="cosine")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--lists", choices=["uniform", "topk"], default="uniform",
+                    help="topk: the top-k lists of bench.py's own tables (dr_score_topk)")
+    ap.add_argument("--after-scan", action="store_true",
+                    help="run the dr_score_topk call before every timed ILD launch "
+                         "(bench.py's step order)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(1)
     n_items, d = args.items, args.dim
-    items = (torch.randn(n_items, d, generator=g, device=dev) / d ** 0.5).to(torch.bfloat16)
-    recs = torch.randint(0, n_items, (args.users, args.k), generator=g, device=dev,
-                         dtype=torch.int32)
+    if args.lists == "topk" or args.after_scan:
+        sys.path.insert(0, ROOT)
+        from bench import gen_table
+        from divrec import ops
+        users = gen_table(args.users, d, 1, dev)
+        items = gen_table(n_items, d, 2, dev)
+    else:
+        items = (torch.randn(n_items, d, generator=g, device=dev) / d ** 0.5).to(torch.bfloat16)
+    if args.lists == "topk":
+        recs = ops.score_topk(users, items, args.k)[1]
+        torch.cuda.synchronize()
+    else:
+        recs = torch.randint(0, n_items, (args.users, args.k), generator=g, device=dev,
+                             dtype=torch.int32)
     tags = args.variants.split(",")
     libs = {t: lib_of(t) for t in tags}
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -80,6 +96,8 @@ def main():
         old = {n: L.dr_get_plan_knob(B.PLAN_KNOBS[n]) for n in kn}
         for n, v in kn.items():
             L.dr_set_plan_knob(B.PLAN_KNOBS[n], v)
+        if args.after_scan:
+            ops.score_topk(users, items, args.k)
         if True:
             e0.record()
             rc = L.dr_ild_embedding(recs.data_ptr(), B.DR_I32, args.users, args.k,
@@ -99,6 +117,7 @@ def main():
             times[t].append(run(t)[0])
     per_user = args.k * 4 + args.k * d * 2 + 4  # int32 lists
     res = {"users": args.users, "k": args.k, "d": d, "items": n_items, "kind": args.kind,
+           "lists": args.lists, "after_scan": args.after_scan,
            "build_id": B.build_id(), "variants": {}}
     bad = False
     for t in tags:
