@@ -678,9 +678,12 @@ Guess guess_for(int64_t n_items, int k, bool split_tail) {
   // 2^16 sample rows are kept (stride 32 up to 2^22 rows, 64 from 4.2M,
   // 128 from 8.4M). Measured with the split tail at 1M x 10M, d = 128:
   // stride 32 / 64 / 128 / 256 = 1912 / 1879 / 1873 / 1880 ms
-  // (profiles/r02_scan/ab_stride_10m.json). Long lists keep stride 32.
+  // (profiles/r02_scan/ab_stride_10m.json). Long lists too since round 6
+  // (k = 1000 at 1M x 10M, lists identical, profiles/r06/k1000_stride/:
+  // stride 32 / 64 / 128 = 1990.8 / 1971.8 / 1963.9 ms; 128 also puts the
+  // sample on the dense tile-max path, 9.8 GB instead of 39 GB at 32).
   g.stride = kGuessStride;
-  while (k < kGuessLongK && g.stride < 128 && n_items / (2 * g.stride) >= 65536) g.stride *= 2;
+  while (g.stride < 128 && n_items / (2 * g.stride) >= 65536) g.stride *= 2;
   if (const int st = knob_int(DR_KNOB_GUESS_STRIDE, 0); st > 1) g.stride = st;  // A/B knob
   // a whole number of 32-row tiles: the sample is stored tile-transposed
   // (sample_rows_kernel), and rows left out only lower the sample's order

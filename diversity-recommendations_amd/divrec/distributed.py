@@ -196,7 +196,7 @@ LAST_TIER_FAILURES = (0, 0)
 def sample_stride(n_items: int, k: int) -> int:
     """The sample stride of dr_score_topk's guess (csrc/score_topk.hip guess_for)."""
     st = 32
-    while k < 256 and st < 128 and n_items // (2 * st) >= 65536:
+    while st < 128 and n_items // (2 * st) >= 65536:
         st *= 2
     return st
 

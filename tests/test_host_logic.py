@@ -224,7 +224,7 @@ def test_global_threshold_helpers():
     assert sample_stride(1_000_000, 100) == 32
     assert sample_stride(5_000_000, 100) == 64
     assert sample_stride(10_000_000, 100) == 128
-    assert sample_stride(10_000_000, 1000) == 32
+    assert sample_stride(10_000_000, 1000) == 128  # long lists too (round 6)
     assert guess_rank(100, 1 / 32) == 17  # the config-2 guess (ks = 17)
     assert guess_rank(100, 78125 / 10_000_000) == 10
     assert guess_rank(5, 0.9) == 5  # never above k

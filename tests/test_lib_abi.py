@@ -212,7 +212,7 @@ def test_headline_plans_on_a_256_cu_device():
     reports no device, and the planner then assumes 256): the headline's
     stride-128 guess with a 6-way split tail over the 4th round's 209 blocks,
     config 2's two unsplit rounds at stride 32, the 8-way shard's stride 32,
-    and k = 1000's stride 32 (tests/test_real_plans.py runs them on the GPU)."""
+    and k = 1000's stride 128 (tests/test_real_plans.py runs them on the GPU)."""
     if torch.cuda.is_available():
         pytest.skip("plans depend on the device's CU count")
     bf = torch.bfloat16
@@ -225,7 +225,7 @@ def test_headline_plans_on_a_256_cu_device():
     assert ops.score_topk_plan(1_000_000, 1_250_000, bf, 128, 100)["sample_stride"] == 32
     assert ops.score_topk_plan(1_000_000, 5_000_000, bf, 128, 100)["sample_stride"] == 64
     p = ops.score_topk_plan(1_000_000, 10_000_000, bf, 128, 1000)
-    assert (p["sample_stride"], p["cap"]) == (32, 2048)
+    assert (p["sample_stride"], p["cap"]) == (128, 2048)
     # long lists: whole-catalog units end compacted to 1024 keys (a 1024-key
     # finalize instead of 2048); 977 blocks on 256 CUs: no split pays here
     assert (p["tail_chunks"], p["head_keys"], p["tail_keys"]) == (1, 1024, 1024)

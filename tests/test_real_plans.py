@@ -129,7 +129,7 @@ def test_forced_stride_split_rescan_exact(d, stride, slots):
 
 
 def test_forced_stride_k1000_split():
-    """k = 1000 (config 5's candidate lists) keeps stride 32 by default; forced
+    """k = 1000 (config 5's candidate lists) at 2^18 rows samples at stride 32; forced
     to 64 with a split tail (long lists split in two): exact."""
     rng = np.random.default_rng(31337)
     d, ni, k = 128, (1 << 18) + 5, 1000
@@ -330,11 +330,12 @@ def test_configs3_eight_way_item_shards_full_size():
 
 def test_config5_plan_1m_x_10m_k1000_then_mmr():
     """BASELINE configs[4] at one GPU, the calls bench.py --workload mmr times:
-    the top-1000 scan of 1M users over the 10M-item catalog (d = 128; stride-32
-    two-tier guess, CAP 2048, long-list flush) and the MMR re-rank of those
-    1000 candidates to 100 on the persistent grid. Integer tables; 60 hot rows
-    at sample positions are the best items of a non-negative user group, whose
-    first-tier (rank 48) and safe (rank 68) thresholds both fall inside the hot
+    the top-1000 scan of 1M users over the 10M-item catalog (d = 128; stride-128
+    two-tier guess on the dense sample path, CAP 2048 with staged survivors,
+    long-list flush) and the MMR re-rank of those 1000 candidates to 100 on
+    the persistent grid. Integer tables; 60 hot rows at sample positions are
+    the best items of a non-negative user group, whose first-tier (rank 17)
+    and safe (rank 28) thresholds both fall inside the hot
     scores: the group goes through every tier down to the -inf rescan. Checked:
     ~600 users from head, split-tail and last blocks plus 100 of the hot group
     against the exact top-1000 (lists and scores); then MMR over all 1M lists:
@@ -343,12 +344,12 @@ def test_config5_plan_1m_x_10m_k1000_then_mmr():
     the last round) replay as valid greedy steps in float64."""
     U_n, I_n, d, k = 1_000_000, 10_000_000, 128, 1000
     plan = ops.score_topk_plan(U_n, I_n, torch.bfloat16, d, k)
-    assert (plan["sample_stride"], plan["cap"], plan["user_blocks"]) == (32, 2048, 977), plan
-    assert (plan["first_tier_rank"], plan["sample_rank"]) == (48, 68), plan
+    assert (plan["sample_stride"], plan["cap"], plan["user_blocks"]) == (128, 2048, 977), plan
+    assert (plan["first_tier_rank"], plan["sample_rank"]) == (17, 28), plan
     rng = np.random.default_rng(5005)
     users = _int_table_dev(U_n, d, 41)
     items = _int_table_dev(I_n, d, 42)
-    items[torch.arange(60, device=DEV) * 32] = 3.0
+    items[torch.arange(60, device=DEV) * 128] = 3.0
     hot = np.unique(rng.choice(U_n, 1000, replace=False))
     hot_t = torch.as_tensor(hot, device=DEV)
     users[hot_t] = users[hot_t].abs()
