@@ -1203,9 +1203,11 @@ def test_score_topk_dense_sample_chunked_units(slots):
     nu, ni, d, k = 70, 32 * 131072 + 45, 32, 300
     U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
     Ut, It = _bf16(U), _bf16(I)
-    plan = ops.score_topk_plan(nu, ni, torch.bfloat16, d, k)
+    # stride 32 forced: k = 300 samples this 4.2M-row catalog at 64 by default
+    knobs = {"guess_stride": 32, **({"scan_slots": slots} if slots else {})}
+    with _backend.plan_knobs(**knobs):
+        plan = ops.score_topk_plan(nu, ni, torch.bfloat16, d, k)
     assert plan["sample_stride"] == 32 and plan["sample_rows"] == 131072
-    knobs = {"scan_slots": slots} if slots else {}
     out = []
     for extra in ({}, {"sample_dense": 0}, {"scan_seed": 0}):
         with _backend.plan_knobs(**knobs, **extra):

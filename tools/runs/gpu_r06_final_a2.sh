@@ -9,6 +9,8 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r06fa
 mkdir -p $O
 cd $R
+timeout -k 10 300 python3 -u -m pytest tests/test_hip_kernels.py -m gpu -k dense_sample_chunked_units -v --timeout 200 --timeout-method thread -p no:cacheprovider > $O/gpu_tests_rerun.log 2>&1
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 timeout -k 10 300 python3 bench.py > $O/bench.jsonl 2> $O/bench.err
 for w in score1m mmr gather bpr fp32 ml100k excl; do
   timeout -k 10 300 python3 bench.py --workload $w --steps 3 --warmup 1 >> $O/workloads.jsonl 2>> $O/workloads.err
