@@ -882,13 +882,19 @@ int launch_embedding(const R* recs, int64_t n_users, int k, const __bf16* E, int
         return DR_EUNSUPPORTED;
     }
   }
-  // the whole list fits in registers for d <= 128 (k <= 128 = 4 tiles):
-  // streamed for k > kStreamMinK, one wave per user below (short lists: the
-  // stream's per-user pipeline overhead dominates; d = 128, 1M users:
-  // k = 10 0.72 against 1.2 ms, k = 40 2.41 against 2.44, k = 64 3.04
-  // against 2.86, profiles/r06/ild_ab/); DR_KNOB_ILD_STREAM forces either
+  // the whole list fits in registers for d <= 128 (k <= 128 = 4 tiles).
+  // Streamed where it wins (profiles/r06/ild_ab/, 1M users over 10M rows):
+  // d = 128 cosine / dot lists longer than kStreamMinK (k = 100 4.4-4.8
+  // against 4.7-5.7 ms, k = 64 2.78 against 2.82-3.04). One wave per user
+  // elsewhere: short lists, where the stream's per-user pipeline overhead
+  // dominates (k = 10 0.72 against 1.14-1.2 ms, k = 40 2.25-2.41 against
+  // 2.32-2.44), d = 64 (2.82-2.96 against 3.07-3.54 ms: half the bytes per
+  // user for the same pipeline), and euclidean (8.6 against 12.0 ms: the
+  // per-pair sqrt on one wave per SIMD). DR_KNOB_ILD_STREAM forces either.
   double sv;
-  const bool stream = dr::plan_knob(DR_KNOB_ILD_STREAM, &sv) ? sv != 0.0 : k > kStreamMinK;
+  const bool stream = dr::plan_knob(DR_KNOB_ILD_STREAM, &sv)
+                          ? sv != 0.0
+                          : d == 128 && kind != DR_ILD_EUCLIDEAN && k > kStreamMinK;
   if (stream && (d == 32 || d == 64 || d == 128)) {
     if (d == 32) launch_stream<R, 32>(recs, n_users, k, E, ni, kind, out, err, s);
     else if (d == 64) launch_stream<R, 64>(recs, n_users, k, E, ni, kind, out, err, s);

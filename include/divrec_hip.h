@@ -66,7 +66,7 @@ enum dr_plan_knob {
   DR_KNOB_GUESS_C1 = 6,     /* set: the offset c1 of that form (z defaults to 3) */
   DR_KNOB_GUESS_TIGHT = 7,  /* 0: one tier (ks1 = ks) */
   DR_KNOB_SAMPLE_DENSE = 8, /* 0: sample scan on compacted key buffers, not dense tile maxima; >1: budget GiB */
-  DR_KNOB_ILD_STREAM = 9,   /* dr_ild_embedding, k <= 128: 0 = one wave per user, 1 = streamed persistent grid (default: streamed for k > 40) */
+  DR_KNOB_ILD_STREAM = 9,   /* dr_ild_embedding, k <= 128: 0 = one wave per user, 1 = streamed persistent grid (default: streamed for d = 128 cosine / dot, k > 40) */
   DR_KNOB_ILD_BUFS = 10,    /* streamed ILD: ring slots (1-KB row pieces) per wave, at least one list's (default: as many as LDS allows) */
   DR_KNOB_COUNT = 11
 };

@@ -770,17 +770,21 @@ def test_ild_embedding_stream_matches_wave_per_user(d, k, rec_dtype):
 
 
 def test_ild_embedding_routes_short_lists_to_the_per_user_kernel():
-    """Default plan: lists of k <= 40 take the one-wave-per-user kernel (faster
-    there), longer ones the streamed kernel: the default output equals the
-    forced kernel's bit for bit on each side of the bound."""
+    """Default plan: d = 128 cosine / dot lists of k > 40 take the streamed
+    kernel; short lists, d = 64 / 32 and euclidean the one-wave-per-user
+    kernel (faster there). The default output equals the forced kernel's
+    bit for bit in each case."""
     rng = np.random.default_rng(40)
-    E = _bf16(oracle.as_bf16_f32(rng.standard_normal((3000, 128)).astype(np.float32)))
-    for k, forced in ((10, 0), (40, 0), (41, 1), (64, 1)):
+    for d, kind, k, forced in ((128, "cosine", 10, 0), (128, "cosine", 40, 0),
+                               (128, "cosine", 41, 1), (128, "dot", 64, 1),
+                               (128, "euclidean", 100, 0), (64, "cosine", 100, 0),
+                               (32, "dot", 100, 0)):
+        E = _bf16(oracle.as_bf16_f32(rng.standard_normal((3000, d)).astype(np.float32)))
         rt = torch.from_numpy(rng.integers(0, 3000, size=(2000, k))).to(DEV)
-        got = ops.ild_embedding(rt, E, "cosine")
+        got = ops.ild_embedding(rt, E, kind)
         with _backend.plan_knobs(ild_stream=forced):
-            ref = ops.ild_embedding(rt, E, "cosine")
-        assert torch.equal(got, ref), k
+            ref = ops.ild_embedding(rt, E, kind)
+        assert torch.equal(got, ref), (d, kind, k)
 
 
 def test_ild_embedding_stream_small_grids():
