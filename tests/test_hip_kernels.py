@@ -577,18 +577,21 @@ def _excl(rng, U, I, nu, ni, n_max=300):
     return frozen
 
 
-@pytest.mark.parametrize("d,k", [(64, 1000), (128, 1000), (128, 1024)])
-def test_score_topk_k1000_guess_exclusion_exact(d, k):
+@pytest.mark.parametrize("d,k,dtype", [(64, 1000, "bf16"), (128, 1000, "bf16"), (128, 1024, "bf16"),
+                                     (64, 1000, "f32")])
+def test_score_topk_k1000_guess_exclusion_exact(d, k, dtype):
     """k = 1000 / 1024 (CAP 2048 candidate buffers, 32-key-per-lane finalize
     sort) over a 2^18+-row catalog, so the guessed-threshold path runs, with
     exclusions: lists and scores equal the oracle (integer tables, exact
-    scores, massive ties)."""
+    scores, massive ties). bf16 d = 128 and fp32 d = 64 (the same 256-B rows)
+    run the staged long-list instance (56-KB stages, round 6)."""
     rng = np.random.default_rng(d + k)
     nu, ni = 24, (1 << 18) + 999
     U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
     frozen = _excl(rng, U, I, nu, ni)
     rowptr, cols = oracle.exclusion_csr(frozen)
-    s, it = ops.score_topk(_bf16(U), _bf16(I), k,
+    t = _f32 if dtype == "f32" else _bf16
+    s, it = ops.score_topk(t(U), t(I), k,
                            exclude=(torch.from_numpy(rowptr).to(DEV), torch.from_numpy(cols).to(DEV)))
     ref_i, ref_s = oracle.recommend_topk(U, I, k, frozen=frozen, return_scores=True)
     assert np.array_equal(it.cpu().numpy().astype(np.int64), ref_i)
