@@ -250,6 +250,41 @@ def test_score_topk_guess_rescan_exact():
     assert np.array_equal(s.cpu().numpy(), ref_s)
 
 
+@pytest.mark.parametrize("k,d,dtype,slots", [(1, 128, "bf16", None), (2, 64, "bf16", 2),
+                                           (5, 32, "f32", None), (1, 64, "f32", 2)])
+def test_score_topk_guess_small_k_exact(k, d, dtype, slots):
+    """The guessed-threshold path at the smallest list lengths (k = 1, 2, 5:
+    the sample's safe rank ks is clipped to k, the first-tier rank to ks),
+    bf16 and fp32 tables, with and without a split plan (scan_slots), users
+    whose single best item is excluded, and duplicate user ids: lists and
+    scores equal the oracle's (integer tables: exact scores, ties by id)."""
+    rng = np.random.default_rng(k * 100 + d)
+    ni = (1 << 18) + 77
+    nu = 2 * (2048 if d <= 64 else 1024) + 35 if slots else 150
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    users = np.concatenate([rng.permutation(nu), rng.integers(0, nu, 20)]).astype(np.int64)
+    sel = np.arange(0, len(users), max(1, len(users) // 120))  # the users checked
+    frozen = [np.zeros(0, np.int64) for _ in users]
+    for n in sel[::2]:
+        frozen[n] = np.argsort(-(I @ U[users[n]]), kind="stable")[:3]  # the best 3 excluded
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    t = _f32 if dtype == "f32" else _bf16
+    knobs = {"scan_slots": slots} if slots else {}
+    with _backend.plan_knobs(**knobs):
+        plan = ops.score_topk_plan(len(users), ni, torch.float32 if dtype == "f32" else torch.bfloat16,
+                                   d, k)
+        s, it = ops.score_topk(t(U), t(I), k, user_ids=torch.from_numpy(users).to(DEV),
+                               exclude=(torch.from_numpy(rowptr).to(DEV),
+                                        torch.from_numpy(cols).to(DEV)))
+    assert plan["sample_stride"] > 0 and plan["sample_rank"] == k
+    if slots:
+        assert plan["tail_chunks"] > 1
+    ref_i, ref_s = oracle.recommend_topk(U, I, k, users=users[sel], frozen=[frozen[n] for n in sel],
+                                         return_scores=True)
+    assert np.array_equal(it.cpu().numpy()[sel].astype(np.int64), ref_i)
+    assert np.array_equal(s.cpu().numpy()[sel], ref_s)
+
+
 @pytest.mark.parametrize("d", [32, 64, 128])
 def test_score_topk_many_workgroups_exact(d):
     """More users than one workgroup holds (2048 at d <= 64, 1024 at d = 128):
