@@ -654,6 +654,11 @@ def main():
         r = None
     if rank == 0:
         with_measured(result["roofline"], dev, "mfma_bf16_tflops")
+        # the ILD's gather against the guide's copy rate and this box's own
+        # float4 copy probe (HBM rates differ from box to box)
+        ild_roof = with_measured(result["ild_roofline"], dev, "hbm_copy_gbs")
+        if ild_roof.get("probe_copy_gbs"):
+            ild_roof["frac_of_probe_copy"] = ild_roof["achieved"] / ild_roof["probe_copy_gbs"]
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(r["users"], r["items"], r["recs"], k,
                                               args.cpu_budget_s)
