@@ -614,6 +614,12 @@ struct TopkArgs {
   int gmax;
   float* tmax;
   int64_t tmax_tiles;
+  // Small catalogs (round 6): the plan made CAP >= n_items, so every key of
+  // the unit fits its buffer and nothing is ever compacted (keep_all = 1):
+  // the finalize sorts all of them. An unseeded scan of a short catalog
+  // otherwise compacted each user's buffer several times from -inf, serially
+  // per wave, while the catalog's few tiles left the MFMA idle.
+  int keep_all;
   // Fallback rescan only: the user count lives on the device (n_users and
   // n_ublocks above are its upper bounds), and pos_map[p] is the caller's
   // position of list entry p (its exclusion row). NULL otherwise.
@@ -695,6 +701,7 @@ __global__ __launch_bounds__(waves_for(W) * 64, waves_for(W) / 4) void score_sca
   // survivor until the first compaction sets a real threshold.
   int flush_at = a.k + a.slack + a.gap;
   flush_at = flush_at < CAP - G::MARGIN ? flush_at : CAP - G::MARGIN;
+  if (a.keep_all) flush_at = 0x7fffffff;  // at most n_items <= CAP keys per buffer
 
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -1442,6 +1449,8 @@ struct Plan {
   int head_keep;        // keys a whole-catalog buffer keeps at its end (0: no end compaction)
   int slack, gap;       // compaction slack and flush gap (TopkArgs)
   int64_t buf_rows;     // candidate buffers: n_users_pad + the tail's extra chunks
+  int keep_all;         // TopkArgs::keep_all: CAP >= n_items, no compaction
+  int64_t all_keys;     // keep_all: the keys a buffer ends with (n_items)
   int grid;
   size_t cand_bytes;
   size_t cnt_bytes;

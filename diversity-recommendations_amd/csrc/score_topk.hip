@@ -519,9 +519,32 @@ constexpr bool kHeadKeep = true;  // long lists: whole-catalog units end compact
 // and breaks even at 1/128. So a head/tail split is planned only for
 // catalogs the guess can seed (seedable); a grid smaller than the CU count
 // (H = 0) is chunked in any case, as before.
-Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
+// Small catalogs (round 6): with at most kKeepAllItems rows the candidate
+// buffer is sized to hold every row (CAP >= n_items, at most 2048: the finalize
+// sort's bound), so the scan never compacts (TopkArgs::keep_all) and the
+// finalize sorts all keys. Config 1's 943 users x 1682 rows ran ONE
+// workgroup whose waves compacted each user's buffer several times from -inf.
+// Measured against the compacting plan (lists identical,
+// profiles/r06/keep_all/): 943 x 1682 d = 32 3.40 -> 1.55 ms, d = 64 2.07 ->
+// 1.56, 10K x 2000 k = 100 4.18 -> 2.07; config 1's whole evaluation step
+// 9.09 -> 5.23 ms. The 2048-key finalize per user grows with the users
+// (60K x 2048 k = 10: 2.35 -> 3.30 ms, break-even near 20K), so the rule
+// takes calls of at most kKeepAllUsers users. Unseeded main scans only (the
+// caller says so: allow_keep_all).
+constexpr bool kKeepAll = true;
+constexpr int64_t kKeepAllItems = 2048;
+constexpr int64_t kKeepAllUsers = 16384;
+
+Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable,
+               bool allow_keep_all = false) {
   Plan p{};
   p.cap = cap_for(w, k);
+  if (kKeepAll && allow_keep_all && !seedable && p.cap > 0 && n_items <= kKeepAllItems &&
+      n_users <= kKeepAllUsers && w <= 256) {  // CAP-2048 instances exist for w <= 256
+    p.keep_all = 1;
+    p.all_keys = n_items;
+    while (p.cap < n_items) p.cap <<= 1;
+  }
   p.users_per_wg = nut_for(w) * 32 * waves_for(w);
   p.n_ublocks = dr::ceil_div(n_users, p.users_per_wg);
   p.n_users_pad = p.n_ublocks * p.users_per_wg;
@@ -544,6 +567,7 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
   double best = (double)H / slots + (double)dr::ceil_div(T, slots);
   int max_c = max_c_override > 0 ? max_c_override : kMaxTailChunks;
   if (const int c = knob_int(DR_KNOB_SCAN_SPLIT, 0); c != 0) max_c = c > 0 ? c : 1;  // A/B knob
+  if (p.keep_all) max_c = 1;  // one unit per user block holds every key
   // a head user's finalize already sorts 2048 keys when its flush bound
   // passes 1024 (k >= ~800): the tail may then gather as many
   const int head_flush = std::min(k + kSlack + kFlushGap, p.cap - (int)stage_items);
@@ -593,6 +617,8 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable) {
 // each stage end, the last included), so k = 100 sorts 256 keys, not CAP = 512
 // (the sort instances start at 256 keys).
 int flush_keys(const Plan& p, int w, int k) {
+  // never compacted: every row's key (and rank k reached: every output slot written)
+  if (p.keep_all) return (int)std::max<int64_t>(p.all_keys, k);
   const int f = k + p.slack + p.gap;
   const int m = p.cap - (int)stage_items_for(w, p.cap);
   return f < m ? f : m;
@@ -757,7 +783,7 @@ struct Layout {
 
 Layout make_layout(int64_t n_users, int64_t n_items, int w, int k) {
   Layout L{};
-  L.main = make_plan(n_users, n_items, w, k, kGuess && n_items >= kGuessMinItems);
+  L.main = make_plan(n_users, n_items, w, k, kGuess && n_items >= kGuessMinItems, true);
   L.g = guess_for(n_items, k, L.main.tail_chunks > 1);
   L.cand = L.main.cand_bytes;
   L.cnt = L.main.cnt_bytes;
@@ -975,6 +1001,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   a.head_keep = p.head_keep;
   a.slack = p.slack;
   a.gap = p.gap;
+  a.keep_all = p.keep_all;  // the main scan only (small catalogs: no guess, no rescans)
   a.init_thr = nullptr;
   a.n_users_dev = nullptr;
   a.pos_map = nullptr;
@@ -1067,6 +1094,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   as.head_keep = ps.head_keep;
   as.slack = ps.slack;
   as.gap = ps.gap;
+  as.keep_all = 0;
   as.gmax = L.dense ? 2 : kSampleGmax;
   as.tmax = (float*)ws;  // the candidate region
   as.tmax_tiles = L.g.S / kTileItems;
@@ -1121,6 +1149,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
     a2.n_users_dev = fcnt;
     a2.n_head = 0;
     a2.end_keep = 0;
+    a2.keep_all = 0;
     a2.dev_split = kMaxRescanChunks;
     a2.buf_blocks = p.buf_rows / p.users_per_wg;
     a2.diag = nullptr;
@@ -1156,6 +1185,7 @@ extern "C" int dr_score_topk(const void* user_table, const int64_t* user_ids, in
   af.tail_chunks = 1;
   af.chunk_items = n_items;
   af.end_keep = 0;
+  af.keep_all = 0;
   af.diag = nullptr;
   DR_SCAN_OR_FAIL(p, af, false)
   DR_CHECK_LAUNCH();

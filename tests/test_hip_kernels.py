@@ -250,6 +250,36 @@ def test_score_topk_guess_rescan_exact():
     assert np.array_equal(s.cpu().numpy(), ref_s)
 
 
+@pytest.mark.parametrize("nu,ni,d,k,dtype", [(300, 300, 64, 600, "bf16"), (70, 2048, 128, 100, "f32"),
+                                            (16384, 1000, 32, 20, "bf16"), (500, 1, 64, 5, "f32")])
+def test_score_topk_small_catalog_keeps_every_key(nu, ni, d, k, dtype):
+    """Small catalogs keep every key (round 6: CAP >= n_items, no compaction,
+    the finalize sorts all of them): k above the catalog (the list's tail is
+    item -1 / score -inf), exactly 2048 rows, the 16384-user bound, a
+    one-row catalog; best items excluded for some users. Exact against the
+    oracle (integer tables)."""
+    rng = np.random.default_rng(nu + ni + k)
+    U, I = _int_table(rng, nu, d), _int_table(rng, ni, d)
+    t = _f32 if dtype == "f32" else _bf16
+    plan = ops.score_topk_plan(nu, ni, torch.float32 if dtype == "f32" else torch.bfloat16, d, k)
+    assert plan["cap"] >= ni and plan["head_keys"] >= max(ni, k)
+    sel = np.unique(np.concatenate([np.arange(0, nu, max(1, nu // 97)), [nu - 1]]))
+    frozen = [np.zeros(0, np.int64) for _ in range(nu)]
+    for n in sel[::3]:
+        frozen[n] = np.argsort(-(I @ U[n]), kind="stable")[:min(5, ni - 1)]
+    rowptr, cols = oracle.exclusion_csr(frozen)
+    s, it = ops.score_topk(t(U), t(I), k, exclude=(torch.from_numpy(rowptr).to(DEV),
+                                                 torch.from_numpy(cols).to(DEV)))
+    got_i, got_s = it.cpu().numpy()[sel], s.cpu().numpy()[sel]
+    for r, n in enumerate(sel):  # one user at a time: list lengths differ when k > candidates
+        ref_i, ref_s = oracle.recommend_topk(U, I, k, users=[n], frozen=[frozen[n]],
+                                             return_scores=True)
+        m = ref_i.shape[1]  # min(k, candidates)
+        assert np.array_equal(got_i[r, :m].astype(np.int64), ref_i[0])
+        assert np.array_equal(got_s[r, :m], ref_s[0])
+        assert (got_i[r, m:] == -1).all() and np.isneginf(got_s[r, m:]).all()
+
+
 @pytest.mark.parametrize("k,d,dtype,slots", [(1, 128, "bf16", None), (2, 64, "bf16", 2),
                                            (5, 32, "f32", None), (1, 64, "f32", 2)])
 def test_score_topk_guess_small_k_exact(k, d, dtype, slots):

@@ -277,3 +277,21 @@ def test_staged_scans_take_catalogs_above_2_28_rows():
         rc = lib.dr_score_topk(None, None, 64, None, n, 0, dtype, d, 10, None, None, None, None,
                                None, 0, None)
         assert rc == -1 and b"null pointer" in lib.dr_last_error()
+
+
+def test_small_catalogs_keep_every_key():
+    """Small catalogs (<= 2048 rows) of calls with at most 16384 users plan a
+    candidate buffer that holds every row (CAP >= n_items), so the scan never
+    compacts and the finalize sorts all keys (round 6; config 1's 943 x 1682
+    shape). Larger calls keep the compacting plan."""
+    f32, bf = torch.float32, torch.bfloat16
+    p = ops.score_topk_plan(943, 1682, f32, 32, 10)
+    assert (p["cap"], p["tail_chunks"], p["head_keys"], p["sample_stride"]) == (2048, 1, 1682, 0)
+    p = ops.score_topk_plan(16384, 500, bf, 128, 100)
+    assert (p["cap"], p["head_keys"]) == (512, 500)
+    assert ops.score_topk_plan(16385, 500, bf, 128, 100)["head_keys"] != 500  # too many users
+    assert ops.score_topk_plan(943, 2049, bf, 64, 10)["cap"] == 1024  # too many rows
+    p = ops.score_topk_plan(100, 300, bf, 64, 600)  # k above the catalog: rank k still reached
+    assert p["head_keys"] >= 600
+    # bf16 d = 512 has no CAP-2048 instance: compacting plan
+    assert ops.score_topk_plan(943, 1682, bf, 512, 10)["cap"] < 2048
