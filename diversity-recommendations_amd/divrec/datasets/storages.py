@@ -89,10 +89,25 @@ class UserItemInteractionsDataset:
     def user_item_csr(self, n_users: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """Per-user sorted, de-duplicated item ids as CSR (rowptr int64
         [n_users+1], items int32): the exclusion lists / positives the GPU
-        kernels consume in place of the reference's per-user Python set ops."""
+        kernels consume in place of the reference's per-user Python set ops.
+
+        The CSR is kept between calls (an evaluation loop asks for the same
+        exclusions every epoch) and rebuilt when the interactions change: the
+        key is the tensor's storage, shape, version and two O(N) checksums of
+        its values, so in-place writes torch does not record (``.data``, numpy
+        views) are seen too. Treat the returned tensors as read-only."""
         n_users = self.number_of_users if n_users is None else n_users
         if self.interactions is None or self.interactions.numel() == 0:
             return torch.zeros(n_users + 1, dtype=torch.int64), torch.zeros(0, dtype=torch.int32)
+        key = _csr_key(self.interactions, n_users)
+        cached = getattr(self, "_csr_cache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        out = self._build_user_item_csr(n_users)
+        self._csr_cache = (key, out)
+        return out
+
+    def _build_user_item_csr(self, n_users: int) -> Tuple[torch.Tensor, torch.Tensor]:
         inter = self.interactions.to(torch.int64)
         inter = inter[inter[:, 0] < n_users]
         # one sorted, de-duplicated 1-D key per (user, item): the same order as
@@ -104,6 +119,15 @@ class UserItemInteractionsDataset:
         rowptr = torch.zeros(n_users + 1, dtype=torch.int64)
         rowptr[1:] = torch.cumsum(counts, 0)
         return rowptr, items.to(torch.int32).contiguous()
+
+
+def _csr_key(inter: torch.Tensor, n_users: int):
+    """Identity of an interactions tensor's values for user_item_csr's cache."""
+    x = inter.to(torch.int64)
+    h1 = int(x.sum())
+    h2 = int((x[:, 0] * 1000003 + x[:, 1] * 7919 + 1).mul_(
+        torch.arange(1, x.size(0) + 1, dtype=torch.int64)).sum())  # order-sensitive
+    return (n_users, inter.data_ptr(), tuple(inter.shape), inter.dtype, inter._version, h1, h2)
 
 
 def get_user_features(data: UserItemInteractionsDataset, user_id: int) -> Optional[torch.Tensor]:

@@ -32,6 +32,7 @@ from divrec.losses import (
     RecommendationsAwareLoss,
 )
 from divrec.metrics import AUCScore
+from divrec.metrics import _rank
 from divrec.models import MatrixFactorization, RankingModel
 
 
@@ -142,7 +143,10 @@ def recommendations_score_loop(dataset: RankingDataset, model: RankingModel,
     model.eval()
     interactions = dataset.data.interactions
     recommendations = get_model_recommendations(dataset, model, number_of_recommendations)
-    return [loss(interactions, recommendations) for loss in losses]
+    # P@k / R@k / MAP@k / NDCG@k of one (interactions, recommendations) pair
+    # come from one dr_rank_metrics launch
+    with _rank.shared_rank_metrics():
+        return [loss(interactions, recommendations) for loss in losses]
 
 
 # --------------------------------------------------------------------------- training

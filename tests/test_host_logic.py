@@ -297,3 +297,53 @@ def test_embedding_distance_device_copy_follows_its_table():
     D.refresh()
     t3 = D.table(cpu)
     assert t3 is not t2 and float(t3[0, 0]) == 5.0
+
+
+def test_user_item_csr_cache_follows_the_interactions():
+    """UserItemInteractionsDataset.user_item_csr keeps its CSR between calls
+    and rebuilds it when the interactions change, including writes torch does
+    not record (.data, a numpy view): the key holds value checksums."""
+    import torch
+    from divrec.datasets import UserItemInteractionsDataset
+
+    inter = torch.tensor([[0, 3], [0, 1], [2, 2], [1, 0], [0, 1]], dtype=torch.int64)
+    ds = UserItemInteractionsDataset(inter.clone(), number_of_users=3, number_of_items=4)
+    a = ds.user_item_csr()
+    assert a[0].tolist() == [0, 2, 3, 4] and a[1].tolist() == [1, 3, 0, 2]
+    assert ds.user_item_csr() is a  # cached
+    ds.interactions.data[4, 1] = 2  # unrecorded write: (0, 1) duplicate -> (0, 2)
+    b = ds.user_item_csr()
+    assert b is not a and b[0].tolist() == [0, 3, 4, 5] and b[1].tolist() == [1, 2, 3, 0, 2]
+    ds.interactions.numpy()[3, 0] = 2  # numpy view: user 1's item moves to user 2
+    c = ds.user_item_csr()
+    assert c[0].tolist() == [0, 3, 3, 5] and c[1].tolist() == [1, 2, 3, 0, 2]
+    assert ds.user_item_csr(2)[0].tolist() == [0, 3, 3]  # another n_users: another key
+
+
+def test_rank_metrics_shared_inside_an_evaluation_loop(monkeypatch):
+    """Inside shared_rank_metrics() the four accuracy metrics of one
+    (interactions, recommendations) pair come from ONE dr_rank_metrics call
+    (train.recommendations_score_loop opens the block); outside it every call
+    computes. Host logic: the kernel call is replaced by a counter."""
+    import torch
+    from divrec import _backend
+    from divrec.metrics import _rank
+
+    calls = []
+
+    def fake(recs, rowptr, items):
+        calls.append(1)
+        n = recs.size(0)
+        return tuple(torch.full((n,), float(i)) for i in range(4))
+
+    monkeypatch.setattr(_backend, "default_device", lambda: torch.device("cpu"))
+    monkeypatch.setattr(_rank.ops, "rank_metrics", fake)
+    inter = torch.tensor([[0, 1], [1, 2]])
+    recs = torch.tensor([[1, 2], [2, 0]])
+    with _rank.shared_rank_metrics():
+        r1 = _rank.rank_metrics(inter, recs)
+        r2 = _rank.rank_metrics(inter, recs)
+        _rank.rank_metrics(inter, recs.clone())  # another tensor: computed
+    assert r1 is r2 and len(calls) == 2
+    _rank.rank_metrics(inter, recs)
+    assert len(calls) == 3
