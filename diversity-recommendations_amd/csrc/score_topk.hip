@@ -529,8 +529,11 @@ constexpr bool kHeadKeep = true;  // long lists: whole-catalog units end compact
 // 1.56, 10K x 2000 k = 100 4.18 -> 2.07; config 1's whole evaluation step
 // 9.09 -> 5.23 ms. The 2048-key finalize per user grows with the users
 // (60K x 2048 k = 10: 2.35 -> 3.30 ms, break-even near 20K), so the rule
-// takes calls of at most kKeepAllUsers users. Unseeded main scans only (the
-// caller says so: allow_keep_all).
+// takes calls of at most kKeepAllUsers users. Such calls have few user
+// blocks, so their catalog is split into stage-long chunks over more CUs (no
+// chunk compacts; the finalize gathers every chunk's keys): 943 x 1682 d = 64
+// 1.55 -> 0.86 ms, 10K x 2000 k = 100 2.05 -> 1.10, config 1's step 3.17 ->
+// 2.43 ms. Unseeded main scans only (the caller says so: allow_keep_all).
 constexpr bool kKeepAll = true;
 constexpr int64_t kKeepAllItems = 2048;
 constexpr int64_t kKeepAllUsers = 16384;
@@ -560,14 +563,17 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable,
   // Shorter chunks lose: every chunk compacts each of its users once at its
   // end (~0.9 ms per workgroup), which config 1's 1682-row catalog split in 3
   // paid (5.1 -> 6.0 ms).
-  const int64_t min_chunk = H > 0 ? 65536 : std::max<int64_t>(stage_items, 8192);
+  // keep-all plans (small catalogs, no compaction) split down to one stage
+  // per chunk: no chunk pays an end compaction, and the few user blocks of
+  // such a call would otherwise scan on as many CUs
+  const int64_t min_chunk = p.keep_all ? stage_items
+                          : H > 0 ? 65536 : std::max<int64_t>(stage_items, 8192);
   if (H > 0 && !seedable) max_c_override = 1;
   const int64_t T = B - H;
   int best_c = 1;
   double best = (double)H / slots + (double)dr::ceil_div(T, slots);
   int max_c = max_c_override > 0 ? max_c_override : kMaxTailChunks;
   if (const int c = knob_int(DR_KNOB_SCAN_SPLIT, 0); c != 0) max_c = c > 0 ? c : 1;  // A/B knob
-  if (p.keep_all) max_c = 1;  // one unit per user block holds every key
   // a head user's finalize already sorts 2048 keys when its flush bound
   // passes 1024 (k >= ~800): the tail may then gather as many
   const int head_flush = std::min(k + kSlack + kFlushGap, p.cap - (int)stage_items);
@@ -575,7 +581,7 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable,
   if (const int m = knob_int(DR_KNOB_TAIL_KEYS, 0); m > 0) max_keys = m;  // A/B knob
   for (int c = 2; c <= max_c && T > 0; ++c) {
     if (n_items / c < min_chunk) break;
-    if (c * k > max_keys) break;  // each chunk keeps at least k keys
+    if (!p.keep_all && c * k > max_keys) break;  // each chunk keeps at least k keys
     const double t = (double)H / slots + (double)dr::ceil_div(T * c, slots) / c;
     if (t < best * 0.99) {  // a smaller split unless a larger one gains > 1 %
       best = t;
@@ -597,7 +603,7 @@ Plan make_plan(int64_t n_users, int64_t n_items, int w, int k, bool seedable,
                                                      : kFlushGap;
   // a tail chunk ends with at most end_keep >= k keys, so c of them fit the
   // finalize's max_keys
-  p.end_keep = best_c > 1 ? std::min(k + kSlack, max_keys / best_c) : 0;
+  p.end_keep = best_c > 1 && !p.keep_all ? std::min(k + kSlack, max_keys / best_c) : 0;
   // Long lists (the flush bound above 1024 keys): every whole-catalog unit ends
   // with a compaction to at most kMaxTailKeys keys (slack kMaxTailKeys - k), so
   // the finalize sorts 1024 keys per user instead of 2048 (k = 1000: the
@@ -629,6 +635,9 @@ int head_keys(const Plan& p, int w, int k) {
 }
 int tail_keys(const Plan& p, int w, int k) {
   if (p.tail_chunks <= 1) return head_keys(p, w, k);
+  // keep-all chunks are never compacted (not even to head_keep): all their
+  // keys, at most n_items <= 2048 over the chunks
+  if (p.keep_all) return std::max(256, flush_keys(p, w, k));
   const int n = p.tail_chunks * p.end_keep;
   return n > 256 ? n : 256;
 }

@@ -283,15 +283,20 @@ def test_small_catalogs_keep_every_key():
     """Small catalogs (<= 2048 rows) of calls with at most 16384 users plan a
     candidate buffer that holds every row (CAP >= n_items), so the scan never
     compacts and the finalize sorts all keys (round 6; config 1's 943 x 1682
-    shape). Larger calls keep the compacting plan."""
+    shape), and split the catalog into stage-long chunks over more CUs.
+    Larger calls keep the compacting plan."""
     f32, bf = torch.float32, torch.bfloat16
     p = ops.score_topk_plan(943, 1682, f32, 32, 10)
-    assert (p["cap"], p["tail_chunks"], p["head_keys"], p["sample_stride"]) == (2048, 1, 1682, 0)
+    assert (p["cap"], p["head_keys"], p["tail_keys"], p["sample_stride"]) == (2048, 1682, 1682, 0)
+    # the one user block's catalog split into stage-long chunks (no chunk compacts)
+    assert (p["head_blocks"], p["tail_chunks"], p["chunk_items"]) == (0, 3, 896)
     p = ops.score_topk_plan(16384, 500, bf, 128, 100)
     assert (p["cap"], p["head_keys"]) == (512, 500)
     assert ops.score_topk_plan(16385, 500, bf, 128, 100)["head_keys"] != 500  # too many users
     assert ops.score_topk_plan(943, 2049, bf, 64, 10)["cap"] == 1024  # too many rows
     p = ops.score_topk_plan(100, 300, bf, 64, 600)  # k above the catalog: rank k still reached
-    assert p["head_keys"] >= 600
+    assert p["head_keys"] >= 600 and p["tail_keys"] >= 600
+    p = ops.score_topk_plan(300, 2000, bf, 128, 1000)  # long lists: split chunks gather every key
+    assert p["tail_chunks"] > 1 and p["tail_keys"] == 2000
     # bf16 d = 512 has no CAP-2048 instance: compacting plan
     assert ops.score_topk_plan(943, 1682, bf, 512, 10)["cap"] < 2048
