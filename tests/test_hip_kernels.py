@@ -167,7 +167,7 @@ def test_gather_dot_backward(d):
 
 
 # --------------------------------------------------------------------------- score_topk
-@pytest.mark.parametrize("d", [32, 64, 128, 256])
+@pytest.mark.parametrize("d", [32, 64, 128, 256, 512])  # 512: the compacting plan (no CAP-2048 instance)
 @pytest.mark.parametrize("k", [1, 10, 100])
 def test_score_topk_integer_exact(d, k):
     rng = np.random.default_rng(1000 * d + k)
